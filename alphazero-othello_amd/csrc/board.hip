@@ -1,0 +1,196 @@
+// board.hip — stateless batched board step / legal-mask / D4 entry points.
+//
+// oth_step_gpu is the north-star kernel: tens of millions of independent positions in
+// SoA (own u64[n], opp u64[n], act u8[n]) -> (own' u64, opp' u64, legal u64, status u16),
+// 43 algorithmic bytes per position.  The host entry points run the same bitboard.h
+// code so single-position Python calls (OthelloGameNew API) and the device agree bit for
+// bit.
+#include <stdexcept>
+#include <string>
+
+#include "bitboard.h"
+#include "common.h"
+
+namespace azc {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+}  // namespace azc
+
+// ------------------------------- device kernels --------------------------------------
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// One position per lane per iteration, grid-stride.  Every global access is a
+// lane-contiguous 8-byte (own/opp/legal), 1-byte (act) or 2-byte (status) access, so a
+// wave moves 64 consecutive positions per instruction.
+__global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ own,
+                                                 const uint64_t* __restrict__ opp,
+                                                 const uint8_t* __restrict__ act,
+                                                 uint64_t* __restrict__ own_o,
+                                                 uint64_t* __restrict__ opp_o,
+                                                 uint64_t* __restrict__ legal_o,
+                                                 uint16_t* __restrict__ status_o,
+                                                 int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const azb::Step s = azb::step(own[i], opp[i], act[i]);
+    own_o[i] = s.own;
+    opp_o[i] = s.opp;
+    legal_o[i] = s.legal;
+    status_o[i] = s.status;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_legal(const uint64_t* __restrict__ own,
+                                                  const uint64_t* __restrict__ opp,
+                                                  uint64_t* __restrict__ legal_o, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    legal_o[i] = azb::legal(own[i], opp[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_d4(const uint64_t* __restrict__ x,
+                                               const uint8_t* __restrict__ sym,
+                                               uint64_t* __restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    out[i] = azb::d4(x[i], sym[i] & 7);
+}
+
+unsigned grid_for(int64_t n) {
+  // enough waves to cover the chip many times over; grid-stride for the rest
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  const int64_t cap = 256 * 32;  // 256 CUs x 32 blocks
+  return (unsigned)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
+}
+
+}  // namespace
+
+// ------------------------------- C ABI: host ------------------------------------------
+
+extern "C" {
+
+const char* az_last_error(void) { return azc::g_last_error.c_str(); }
+int az_abi_version(void) { return AZ_ABI_VERSION; }
+
+int oth_legal_cpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_legal_cpu: n=%lld < 0", (long long)n);
+  AZ_REQUIRE(n == 0 || (own && opp && legal_o), AZ_ERR_ARG, "oth_legal_cpu: null buffer");
+  for (int64_t i = 0; i < n; ++i) legal_o[i] = azb::legal(own[i], opp[i]);
+  return AZ_OK;
+}
+
+int oth_step_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                 uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                 int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_step_cpu: n=%lld < 0", (long long)n);
+  AZ_REQUIRE(n == 0 || (own && opp && act && own_o && opp_o && legal_o && status_o),
+             AZ_ERR_ARG, "oth_step_cpu: null buffer");
+  int64_t first_bad = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const azb::Step s = azb::step(own[i], opp[i], act[i]);
+    own_o[i] = s.own;
+    opp_o[i] = s.opp;
+    legal_o[i] = s.legal;
+    status_o[i] = s.status;
+    if ((s.status & azb::kFlagIllegal) && first_bad < 0) first_bad = i;
+  }
+  if (first_bad >= 0)
+    return azc::set_error(AZ_ERR_ILLEGAL, "Illegal move: %d (position %lld)",
+                          (int)act[first_bad], (long long)first_bad);
+  return AZ_OK;
+}
+
+int oth_pack_np(const int8_t* states, const int8_t* player, uint64_t* own, uint64_t* opp,
+                int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_pack_np: n < 0");
+  AZ_REQUIRE(n == 0 || (states && player && own && opp), AZ_ERR_ARG,
+             "oth_pack_np: null buffer");
+  for (int64_t i = 0; i < n; ++i) {
+    const int8_t* s = states + 64 * i;
+    const int p = player[i];
+    uint64_t a = 0, b = 0;
+    for (int k = 0; k < 64; ++k) {
+      a |= (uint64_t)(s[k] == p) << k;
+      b |= (uint64_t)(s[k] == -p) << k;
+    }
+    own[i] = a;
+    opp[i] = b;
+  }
+  return AZ_OK;
+}
+
+int oth_unpack_np(const uint64_t* own, const uint64_t* opp, const int8_t* player,
+                  int8_t* states, int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_unpack_np: n < 0");
+  AZ_REQUIRE(n == 0 || (own && opp && player && states), AZ_ERR_ARG,
+             "oth_unpack_np: null buffer");
+  for (int64_t i = 0; i < n; ++i) {
+    int8_t* s = states + 64 * i;
+    const int8_t p = player[i];
+    for (int k = 0; k < 64; ++k) {
+      const int8_t v = (int8_t)(((own[i] >> k) & 1) ? p : (((opp[i] >> k) & 1) ? -p : 0));
+      s[k] = v;
+    }
+  }
+  return AZ_OK;
+}
+
+int oth_d4_cpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_d4_cpu: n < 0");
+  AZ_REQUIRE(n == 0 || (x && sym && out), AZ_ERR_ARG, "oth_d4_cpu: null buffer");
+  for (int64_t i = 0; i < n; ++i) out[i] = azb::d4(x[i], sym[i] & 7);
+  return AZ_OK;
+}
+
+// ------------------------------- C ABI: device ----------------------------------------
+
+int oth_legal_gpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n,
+                  void* stream) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_legal_gpu: n < 0");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(own && opp && legal_o, AZ_ERR_ARG, "oth_legal_gpu: null buffer");
+  hipLaunchKernelGGL(k_legal, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
+                     own, opp, legal_o, n);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                 uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                 int64_t n, void* stream) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_step_gpu: n < 0");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(own && opp && act && own_o && opp_o && legal_o && status_o, AZ_ERR_ARG,
+             "oth_step_gpu: null buffer");
+  hipLaunchKernelGGL(k_step, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
+                     own, opp, act, own_o, opp_o, legal_o, status_o, n);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int oth_d4_gpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n,
+               void* stream) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_d4_gpu: n < 0");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(x && sym && out, AZ_ERR_ARG, "oth_d4_gpu: null buffer");
+  hipLaunchKernelGGL(k_d4, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream), x,
+                     sym, out, n);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,204 @@
+/* az_othello.h — C ABI of the MI355X-native Othello self-play engine.
+ *
+ * The reference (AfoninAndrei/alphaZero-Othello) is pure Python and has no FFI; its
+ * drop-in surfaces are duck-typed Python classes.  Every entry point below replaces a
+ * reference Python routine, cited as file:line into the reference tree.  The Python
+ * host side (alphazero-othello_amd/envs, MCTS_model.py, self_play_worker.py) binds
+ * these through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - every function returns int: AZ_OK (0) or a negative AZ_ERR_* code; az_last_error()
+ *     returns a thread-local message for the last failure on the calling thread.  No C++
+ *     exception crosses the ABI.
+ *   - buffers are caller-owned.  *_cpu functions take host pointers and are reentrant
+ *     and stateless.  *_gpu functions take device pointers and are asynchronous on the
+ *     given hipStream_t (passed as void*; NULL = the legacy default stream).
+ *   - bitboard layout: bit r*8+c <-> square (r, c) of the row-major (8,8) state array
+ *     (`_BitBoard` layout, envs/othello.py:202-212).  own = side to move.
+ *   - a board step's status word (uint16): low byte = flags (AZ_FLAG_*), high byte =
+ *     signed disc difference (side to move after the step minus its opponent).
+ *   - an engine handle is NOT thread-safe: one owner thread per engine.
+ */
+#ifndef AZ_OTHELLO_H
+#define AZ_OTHELLO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZ_ABI_VERSION 1
+
+enum {
+  AZ_OK = 0,
+  AZ_ERR_ILLEGAL = -1,  /* illegal placement (reference: ValueError, envs/othello.py:421) */
+  AZ_ERR_ARG = -2,      /* bad argument / shape */
+  AZ_ERR_HIP = -3,      /* HIP runtime failure */
+  AZ_ERR_CAPACITY = -4, /* node arena / trajectory capacity exceeded */
+  AZ_ERR_STATE = -5,    /* engine state does not allow the call (e.g. not a child: KeyError,
+                           MCTS_model.py:214) */
+};
+
+enum {
+  AZ_FLAG_TERMINAL = 1, /* neither side has a placement (envs/othello.py:435-454) */
+  AZ_FLAG_NOPLACE = 2,  /* side to move has no placement: valid mask is {pass} */
+  AZ_FLAG_ILLEGAL = 4,  /* the step's action was illegal; outputs = inputs */
+  AZ_FLAG_PASSED = 8,   /* the step's action was the pass (64) */
+};
+
+const char* az_last_error(void);
+int az_abi_version(void);
+
+/* ---------------- stateless board entry points: host ---------------------------- */
+
+/* legal placements of own vs opp.  Replaces _BitBoard._legal_moves / valid_mask
+ * (envs/othello.py:157-169) and the core of OthelloGameNew.get_valid_moves (:394-411). */
+int oth_legal_cpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n);
+
+/* one board step per position: act in 0..63 (placement) or 64 (pass).  Outputs are the
+ * next side's (own, opp), its legal mask and the status word.  Replaces
+ * OthelloGameNew.get_next_state (envs/othello.py:413-433) + _BitBoard.make_move
+ * (:171-200) + get_value_and_terminated (:435-454) + _BitBoard.score (:214-220).
+ * Returns AZ_ERR_ILLEGAL if any position had an illegal placement (its status carries
+ * AZ_FLAG_ILLEGAL and its outputs equal its inputs); all other positions are valid. */
+int oth_step_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                 uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                 int64_t n);
+
+/* int8 (n,8,8) absolute-colour states + int8 player[n] -> (own, opp) bitboards where
+ * own = stones equal to player.  Replaces OthelloGameNew._np_to_bitboards
+ * (envs/othello.py:358-371) in the row-major layout (no 180-degree rotation). */
+int oth_pack_np(const int8_t* states, const int8_t* player, uint64_t* own, uint64_t* opp,
+                int64_t n);
+
+/* inverse of oth_pack_np: own stones -> player, opp stones -> -player.  Replaces
+ * OthelloGameNew._bitboards_to_np (envs/othello.py:373-388). */
+int oth_unpack_np(const uint64_t* own, const uint64_t* opp, const int8_t* player,
+                  int8_t* states, int64_t n);
+
+/* dihedral transform sym = k + 4*flip (np.rot90 k times, then np.fliplr if flip) of each
+ * bitboard.  Replaces the D4 maps of get_random_symmetry (envs/othello.py:501-526) and
+ * random_symmetry (MCTS_model.py:15-28). */
+int oth_d4_cpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n);
+
+/* ---------------- stateless board entry points: device --------------------------- */
+int oth_legal_gpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n,
+                  void* stream);
+int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                 uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                 int64_t n, void* stream);
+int oth_d4_gpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n,
+               void* stream);
+
+/* ---------------- batched MCTS self-play engine (device) -------------------------
+ * G game slots, each with its own flat SoA node arena (tree of reference `Node`s,
+ * MCTS_model.py:46-169) and trajectory buffer.  One sim-step = az_select (descend every
+ * game's tree to one leaf, PUCT of MCTS_model.py:129-139 / :362-370; terminal leaves are
+ * backed up in place) -> caller evaluates the leaves (policy/value net) -> az_expand_backup
+ * (MCTS_model.py:325-360 eager expansion + backup :160-169).  With one leaf per game per
+ * step the search is exactly the reference with args['num_threads'] = 1. */
+
+typedef struct az_engine az_engine;
+
+enum { AZ_EVAL_EXTERNAL = 0, AZ_EVAL_ROLLOUT = 1 };
+enum { AZ_RNG_DEVICE = 0, AZ_RNG_INJECTED = 1 };
+enum { AZ_GAME_IDLE = 0, AZ_GAME_ACTIVE = 1, AZ_GAME_FINISHED = 2 };
+
+typedef struct az_config {
+  int32_t n_games;               /* G concurrent game slots */
+  int32_t node_capacity;         /* arena nodes per game (0 -> 16384) */
+  int32_t max_plies;             /* trajectory capacity per game (0 -> 128) */
+  int32_t num_simulations;       /* args['num_simulations'] */
+  double c_puct;                 /* args['c_puct'] */
+  double dirichlet_alpha;        /* self_play_worker.py:56 */
+  double dirichlet_epsilon;      /* self_play_worker.py:57; 0 disables root noise */
+  double temperature;            /* args['mcts_temperature'] (self_play_worker.py:61) */
+  int32_t num_exploratory_moves; /* args['num_exploratory_moves'] */
+  double lambd;                  /* args['lambda'] (TD(lambda), self_play_worker.py:8-35) */
+  int32_t eval_mode;             /* AZ_EVAL_EXTERNAL (net) or AZ_EVAL_ROLLOUT (policy None) */
+  int32_t rng_mode;              /* AZ_RNG_DEVICE (Philox) or AZ_RNG_INJECTED (parity) */
+  int32_t d4_augment;            /* 1: random D4 transform per leaf in the NN input pack,
+                                    inverse-mapped priors (config #5) */
+  int32_t refill;                /* 1: finished games restart from the initial position */
+  uint64_t seed;                 /* Philox key */
+  uint64_t stream_id;            /* Philox sub-stream (rank) */
+} az_config;
+
+int az_engine_create(const az_config* cfg, az_engine** out);
+int az_engine_destroy(az_engine* eng);
+
+/* every slot -> a fresh game at the initial position, player +1 (self_play_worker.py:
+ * 55-57).  Synchronous. */
+int az_reset_all(az_engine* eng, void* stream);
+/* slot -> root at an arbitrary position (MCTS.policy_improve_step with root None,
+ * MCTS_model.py:223-228).  Synchronous.  player in {+1,-1}. */
+int az_set_root(az_engine* eng, int32_t slot, uint64_t own, uint64_t opp, int32_t player,
+                void* stream);
+/* start a search: sims counter := 0 for every active slot (MCTS_model.py:237). */
+int az_begin_search(az_engine* eng, int32_t num_simulations, void* stream);
+
+/* one leaf per active slot whose search is not done.  nn_in: float [G,64], the
+ * canonical input player*state (Models.py:16) of the leaf, zeros for slots without a
+ * leaf.  leaf_o (optional, int32 [G]): leaf node index or -1. */
+int az_select(az_engine* eng, float* nn_in, int32_t* leaf_o, void* stream);
+
+/* priors: float [G,65] (softmax output), values: float [G] (tanh output), ignored in
+ * rollout mode.  noise: double [G,65] Dirichlet vectors for AZ_RNG_INJECTED (may be NULL
+ * when epsilon is 0).  Expands every pending leaf and backs up its value. */
+int az_expand_backup(az_engine* eng, const float* priors, const float* values,
+                     const double* noise, void* stream);
+
+/* pi from root visit counts (MCTS_model.py:244-274), trajectory record
+ * (self_play_worker.py:67-73), action sample (self_play_worker.py:75).
+ * u_tie/u_act: double [G] uniforms for AZ_RNG_INJECTED (NULL otherwise).
+ * pi_o float [G,65], action_o int32 [G], vroot_o double [G]: optional outputs. */
+int az_root_policy(az_engine* eng, const double* u_tie, const double* u_act, float* pi_o,
+                   int32_t* action_o, double* vroot_o, void* stream);
+
+/* play the chosen (or given, action != NULL: int32 [G], -1 = chosen) action in every
+ * active slot: re-root with subtree reuse (MCTS.make_move, MCTS_model.py:200-215),
+ * terminal check from the mover's view (self_play_worker.py:77-86).  Compacts arenas. */
+int az_advance(az_engine* eng, const int32_t* action, void* stream);
+
+/* finished games -> TD(lambda) targets (get_training_data, self_play_worker.py:8-35)
+ * appended to the device sample buffer; with refill, their slots restart.
+ * Returns (host) the number of games harvested in *n_games_o and total samples in the
+ * device buffer in *n_samples_o.  Synchronous. */
+int az_harvest(az_engine* eng, int32_t* n_games_o, int64_t* n_samples_o, void* stream);
+
+/* device sample buffer (filled by az_harvest): own/opp u64 canonical board (state*player
+ * of the recorded ply), pi float[65], z double, player int8.  Pointers are device
+ * pointers owned by the engine; n <= capacity. */
+int az_samples(az_engine* eng, uint64_t** own, uint64_t** opp, float** pi, double** z,
+               int8_t** player, int64_t* n, int64_t* capacity);
+int az_clear_samples(az_engine* eng);
+
+/* host copies of per-slot state: status (AZ_GAME_*), ply, winner (+1/-1/0), root player,
+ * nodes in use, arena overflow count.  Any pointer may be NULL.  Synchronous. */
+int az_game_info(az_engine* eng, int32_t* status, int32_t* ply, int32_t* winner,
+                 int32_t* root_player, int32_t* n_nodes, int32_t* overflow, void* stream);
+
+/* host copy of one slot's tree (n_nodes entries; root = node 0): bitboards, visit count,
+ * value sum, prior, parent, first child, child count, action, flags (bit0 expanded,
+ * bit1 terminal, bit2 f64 child priors), terminal value.  Any pointer may be NULL. */
+int az_export_tree(az_engine* eng, int32_t slot, int32_t max_nodes, uint64_t* own,
+                   uint64_t* opp, uint64_t* legal, int32_t* N, double* W, double* prior,
+                   int32_t* parent, int32_t* first_child, uint8_t* nchild, uint8_t* action,
+                   uint8_t* flags, int8_t* tval, int32_t* n_nodes_o, void* stream);
+
+/* host copy of one slot's trajectory (ply entries): canonical own/opp, pi, player,
+ * root value.  Synchronous. */
+int az_export_trajectory(az_engine* eng, int32_t slot, int32_t max_plies, uint64_t* own,
+                         uint64_t* opp, float* pi, int8_t* player, double* vroot,
+                         int32_t* n_plies_o, void* stream);
+
+/* re-root one slot on the child reached by `action` (MCTS.make_move,
+ * MCTS_model.py:200-215): AZ_ERR_STATE if the root has no such child (KeyError).
+ * Synchronous. */
+int az_make_move(az_engine* eng, int32_t slot, int32_t action, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AZ_OTHELLO_H */

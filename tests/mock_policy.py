@@ -1,0 +1,61 @@
+"""Deterministic mock policy/value function used by every MCTS parity test.
+
+The reference nets (Models.py) are random-init here (no checkpoints offline), so MCTS
+parity is pinned with a closed-form policy instead.  The function is
+integer arithmetic on the canonical board x = player*state (Models.py:16), so numpy, the
+reference MCTS and the GPU engine's evaluator produce bit-identical priors and values:
+
+    h_a     = 1 + ((A @ (x+1))_a mod 1021)       a in 0..64
+    prior_a = float32(h_a) / 1024                 (exact in float32, NOT normalised:
+                                                   the MCTS masks and renormalises)
+    value   = (((B @ (x+1)) mod 2001) - 1000) / 1024   (exact in float32)
+"""
+import numpy as np
+
+_i = np.arange(65, dtype=np.int64)[:, None]
+_j = np.arange(64, dtype=np.int64)[None, :]
+A = ((_i * 131 + _j * 71 + _i * _j * 7) % 97).astype(np.int64)  # [65, 64]
+B = ((np.arange(64, dtype=np.int64) * 37 + 11) % 89).astype(np.int64)  # [64]
+
+
+def mock_eval(canonical):
+    """canonical: int array [..., 64] with values in {-1, 0, +1}.
+    Returns priors float32 [..., 65] and values float64 [...] (float32-exact)."""
+    x = np.asarray(canonical).astype(np.int64) + 1
+    h = (x @ A.T) % 1021 + 1
+    priors = h.astype(np.float32) / np.float32(1024)
+    k = (x @ B) % 2001
+    values = (k - 1000) / 1024.0
+    return priors, values
+
+
+class MockPolicy:
+    """Duck-typed `policy` for the reference MCTS (policy.inference(state, player))."""
+
+    def inference(self, state, current_player):
+        canon = (current_player * np.asarray(state)).reshape(-1)
+        p, v = mock_eval(canon)
+        return p.astype(np.float32), float(v)
+
+
+class MockPolicyNet(MockPolicy):
+    """Constructible the way one_self_play builds its net (self_play_worker.py:43-46)."""
+
+    def __init__(self, **cfg):
+        pass
+
+    def load_state_dict(self, sd):
+        return None
+
+    def eval(self):
+        return self
+
+    def get_config(self):
+        return {}
+
+
+def mock_eval_planes(nn_in):
+    """Evaluator for the engine: nn_in float [B, 64] canonical planes (+1/-1/0)."""
+    x = np.rint(np.asarray(nn_in, np.float32)).astype(np.int64).reshape(-1, 64)
+    p, v = mock_eval(x)
+    return p, v.astype(np.float32)
