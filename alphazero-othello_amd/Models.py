@@ -1,0 +1,180 @@
+"""Policy/value networks with the reference's module names and state_dict keys
+(reference Models.py:1-221), plus the batched device-side evaluation the engine uses.
+
+The nets are plain PyTorch-ROCm (MIOpen convolutions / hipBLASLt linears on MFMA): the
+only dense contractions on the path.  `Inference.inference` keeps the reference's batch-1
+host API (Models.py:11-31); `evaluate_planes` is what the batched self-play engine calls
+on the [G, 64] canonical planes it packs on device.
+"""
+from typing import Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Inference:
+    """Mixin: batch-1 host inference (reference Models.py:9-31) and batched device
+    inference over packed canonical planes."""
+
+    def inference(self, state: np.ndarray, current_player: int):
+        x = torch.from_numpy((current_player * state).astype(np.float32)).unsqueeze(0)
+        x = x.to(next(self.parameters()).device)
+        self.eval()
+        with torch.no_grad():
+            logits, value = self(x)
+            policy = self.softmax(logits)
+        return policy[0].cpu().numpy(), value[0, 0].cpu().numpy().item()
+
+    @torch.no_grad()
+    def evaluate_planes(self, planes: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """planes: float [B, 64] canonical boards (player*state) -> (softmax priors
+        float32 [B, 65], tanh values float32 [B])."""
+        n = getattr(self, "board_size", 3 if planes.shape[-1] == 9 else 8)
+        x = planes.view(planes.shape[0], 1, n, n)
+        p = next(self.parameters())
+        if x.dtype != p.dtype:
+            x = x.to(p.dtype)
+        logits, value = self(x)
+        return (torch.softmax(logits.float(), dim=-1),
+                value.float().reshape(-1))
+
+
+class TicTacToeNet(nn.Module, Inference):
+    """3x3 MLP (reference Models.py:34-69)."""
+
+    def __init__(self, state_size, output_size):
+        super().__init__()
+        self.action_size = output_size
+        self.fc1 = nn.Linear(state_size, 64)
+        self.fc2 = nn.Linear(64, 64)
+        self.policy_head = nn.Linear(64, output_size)
+        self.value_head = nn.Linear(64, 1)
+        self.softmax = nn.Softmax(dim=-1)
+        self._cfg = {"state_size": state_size, "output_size": output_size}
+
+    def get_config(self):
+        return dict(self._cfg)
+
+    def forward(self, x):
+        h = F.relu(self.fc2(F.relu(self.fc1(x.flatten(start_dim=1)))))
+        return self.policy_head(h), torch.tanh(self.value_head(h))
+
+
+class ResidualBlock(nn.Module):
+    """conv-BN-ReLU-conv-BN + skip, ReLU (reference Models.py:72-90)."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn1 = nn.BatchNorm2d(channels)
+        self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn2 = nn.BatchNorm2d(channels)
+
+    def forward(self, x):
+        y = F.relu(self.bn1(self.conv1(x)))
+        return F.relu(self.bn2(self.conv2(y)) + x)
+
+
+class FastOthelloNet(nn.Module, Inference):
+    """Small net (reference Models.py:93-161): conv stem, one residual block, one extra
+    conv block, FC policy head (65 logits) and a 2-layer FC value head."""
+
+    def __init__(self, board_size: int, action_size: int):
+        super().__init__()
+        self.board_size = board_size
+        self.action_size = action_size
+        self.initial_conv = nn.Sequential(nn.Conv2d(1, 64, kernel_size=3, padding=1),
+                                          nn.BatchNorm2d(64), nn.ReLU())
+        self.res_block = ResidualBlock(64)
+        self.conv_add = nn.Sequential(nn.Conv2d(64, 64, kernel_size=3, padding=1),
+                                      nn.BatchNorm2d(64), nn.ReLU())
+        flat = 64 * board_size * board_size
+        self.fc_policy = nn.Linear(flat, action_size)
+        self.fc_value1 = nn.Linear(flat, 64)
+        self.fc_value2 = nn.Linear(64, 1)
+        self.softmax = nn.Softmax(dim=-1)
+
+    def get_config(self):
+        return {"board_size": self.board_size, "action_size": self.action_size}
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        h = self.conv_add(self.res_block(self.initial_conv(x)))
+        h = h.reshape(h.size(0), -1)
+        value = torch.tanh(self.fc_value2(F.relu(self.fc_value1(h))))
+        return self.fc_policy(h), value
+
+
+class AlphaZeroNet(nn.Module, Inference):
+    """ResNet trunk + AlphaZero heads (reference Models.py:164-221)."""
+
+    def __init__(self, board_size: int, action_size: int, n_res_blocks: int = 5,
+                 channels: int = 128):
+        super().__init__()
+        self.board_size = board_size
+        self.action_size = action_size
+        self.n_res_blocks = n_res_blocks
+        self.channels = channels
+        self.conv0 = nn.Conv2d(1, channels, 3, padding=1, bias=False)
+        self.bn0 = nn.BatchNorm2d(channels)
+        self.res = nn.Sequential(*[ResidualBlock(channels) for _ in range(n_res_blocks)])
+        self.pol_conv = nn.Conv2d(channels, 2, 1, bias=False)
+        self.pol_bn = nn.BatchNorm2d(2)
+        self.pol_fc = nn.Linear(2 * board_size * board_size, action_size)
+        self.val_conv = nn.Conv2d(channels, 1, 1, bias=False)
+        self.val_bn = nn.BatchNorm2d(1)
+        self.val_fc1 = nn.Linear(board_size * board_size, 256)
+        self.val_fc2 = nn.Linear(256, 1)
+        self.softmax = nn.Softmax(dim=-1)
+
+    def get_config(self):
+        return {"board_size": self.board_size, "action_size": self.action_size,
+                "n_res_blocks": self.n_res_blocks, "channels": self.channels}
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        h = self.res(F.relu(self.bn0(self.conv0(x))))
+        p = F.relu(self.pol_bn(self.pol_conv(h)))
+        v = F.relu(self.val_bn(self.val_conv(h)))
+        v = torch.tanh(self.val_fc2(F.relu(self.val_fc1(v.reshape(v.size(0), -1)))))
+        return self.pol_fc(p.reshape(p.size(0), -1)), v
+
+
+def get_config(net):
+    return net.get_config()
+
+
+def inference_copy(net: nn.Module, device, dtype=torch.float32) -> nn.Module:
+    """An eval-mode copy of `net` on `device` for the batched engine: BatchNorm folded
+    into the preceding convolution (same function in eval mode, fewer kernels per step).
+    `dtype` float16 is config #5's fp16 inference."""
+    import copy
+
+    m = copy.deepcopy(net).eval()
+
+    def fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+        w = conv.weight.detach()
+        b = conv.bias.detach() if conv.bias is not None else torch.zeros(w.shape[0])
+        scale = bn.weight.detach() / torch.sqrt(bn.running_var + bn.eps)
+        conv.weight = nn.Parameter(w * scale[:, None, None, None])
+        conv.bias = nn.Parameter((b - bn.running_mean) * scale + bn.bias.detach())
+        return nn.Identity()
+
+    for mod in list(m.modules()):
+        if isinstance(mod, ResidualBlock):
+            mod.bn1 = fold(mod.conv1, mod.bn1)
+            mod.bn2 = fold(mod.conv2, mod.bn2)
+        if isinstance(mod, AlphaZeroNet):
+            mod.bn0 = fold(mod.conv0, mod.bn0)
+            mod.pol_bn = fold(mod.pol_conv, mod.pol_bn)
+            mod.val_bn = fold(mod.val_conv, mod.val_bn)
+        if isinstance(mod, FastOthelloNet):
+            for seq in (mod.initial_conv, mod.conv_add):
+                seq[1] = fold(seq[0], seq[1])
+    m = m.to(device=device, dtype=dtype)
+    m = m.to(memory_format=torch.channels_last)
+    return m.eval()

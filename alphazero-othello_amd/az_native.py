@@ -1,0 +1,224 @@
+"""ctypes binding of the C-ABI library `libaz_othello.so` (include/az_othello.h).
+
+The whole product path goes through this module: the OthelloGameNew drop-in
+(envs/othello.py), the MCTS drop-in (MCTS_model.py) and the batched self-play engine
+(engine.py).  There is no fallback: if the library is missing this module raises on
+import, naming the build command.
+
+Error mapping follows the reference's Python conventions:
+AZ_ERR_ILLEGAL -> ValueError("Illegal move: a") (envs/othello.py:421),
+AZ_ERR_STATE -> KeyError(action) (MCTS_model.py:214), everything else -> RuntimeError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libaz_othello.so")
+
+AZ_OK = 0
+AZ_ERR_ILLEGAL = -1
+AZ_ERR_ARG = -2
+AZ_ERR_HIP = -3
+AZ_ERR_CAPACITY = -4
+AZ_ERR_STATE = -5
+
+AZ_FLAG_TERMINAL = 1
+AZ_FLAG_NOPLACE = 2
+AZ_FLAG_ILLEGAL = 4
+AZ_FLAG_PASSED = 8
+
+AZ_EVAL_EXTERNAL, AZ_EVAL_ROLLOUT = 0, 1
+AZ_RNG_DEVICE, AZ_RNG_INJECTED = 0, 1
+AZ_GAME_IDLE, AZ_GAME_ACTIVE, AZ_GAME_FINISHED, AZ_GAME_SEARCH_DONE = 0, 1, 2, 3
+
+
+class AzConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_games", ctypes.c_int32),
+        ("node_capacity", ctypes.c_int32),
+        ("max_plies", ctypes.c_int32),
+        ("num_simulations", ctypes.c_int32),
+        ("c_puct", ctypes.c_double),
+        ("dirichlet_alpha", ctypes.c_double),
+        ("dirichlet_epsilon", ctypes.c_double),
+        ("temperature", ctypes.c_double),
+        ("num_exploratory_moves", ctypes.c_int32),
+        ("lambd", ctypes.c_double),
+        ("eval_mode", ctypes.c_int32),
+        ("rng_mode", ctypes.c_int32),
+        ("d4_augment", ctypes.c_int32),
+        ("auto_play", ctypes.c_int32),
+        ("refill", ctypes.c_int32),
+        ("sample_capacity", ctypes.c_int64),
+        ("inj_noise_slots", ctypes.c_int32),
+        ("inj_uniform_slots", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("stream_id", ctypes.c_uint64),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_D = ctypes.c_double
+
+# name -> argtypes (restype is int for every entry point except az_last_error)
+SIGNATURES = {
+    "az_abi_version": [],
+    "oth_legal_cpu": [_P, _P, _P, _I64],
+    "oth_step_cpu": [_P, _P, _P, _P, _P, _P, _P, _I64],
+    "oth_make_move_cpu": [_P, _P, _P, _P, _P, _I64],
+    "oth_pack_np": [_P, _P, _P, _P, _I64],
+    "oth_unpack_np": [_P, _P, _P, _P, _I64],
+    "oth_d4_cpu": [_P, _P, _P, _I64],
+    "oth_legal_gpu": [_P, _P, _P, _I64, _P],
+    "oth_step_gpu": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
+    "oth_d4_gpu": [_P, _P, _P, _I64, _P],
+    "az_engine_create": [ctypes.POINTER(AzConfig), ctypes.POINTER(_P)],
+    "az_engine_destroy": [_P],
+    "az_engine_geometry": [_P, _P, _P, _P],
+    "az_reset_all": [_P, _I64, _I32, _P],
+    "az_set_root": [_P, _I32, _U64, _U64, _I32, _P],
+    "az_begin_search": [_P, _I32, _I32, _P],
+    "az_select": [_P, _P, _P, _P],
+    "az_expand_backup": [_P, _P, _P, _P],
+    "az_play": [_P, _P],
+    "az_inject": [_P, _P, _P, _P],
+    "az_root_policy": [_P, _I32, _D, _D, _P, _P, _P, _P],
+    "az_make_move": [_P, _I32, _I32, _P],
+    "az_counters": [_P, _P, _P],
+    "az_game_info": [_P, _P, _P, _P, _P, _P, _P, _P],
+    "az_export_tree": [_P, _I32, _I32] + [_P] * 13,
+    "az_export_trajectory": [_P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
+    "az_samples": [_P, _P, _P, _P, _P, _P, _P, _P],
+    "az_copy_samples": [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "az_clear_samples": [_P, _P],
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` (build()) "
+            "or `python alphazero-othello_amd/az_build.py`; there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.az_last_error.argtypes = []
+    lib.az_last_error.restype = ctypes.c_char_p
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _I
+    return lib
+
+
+lib = _load()
+
+
+def last_error():
+    m = lib.az_last_error()
+    return m.decode() if m else ""
+
+
+def check(rc, what=""):
+    """Raise the reference's exception type for a failed C-ABI call."""
+    if rc == AZ_OK:
+        return
+    msg = last_error()
+    if rc == AZ_ERR_ILLEGAL:
+        raise ValueError(msg or f"Illegal move ({what})")
+    if rc == AZ_ERR_STATE:
+        try:
+            key = int(msg.split(":")[0])
+        except ValueError:
+            key = msg
+        raise KeyError(key)
+    raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(a):
+    """Host numpy array or device torch tensor -> void*."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"], "buffer must be C-contiguous"
+        return a.ctypes.data_as(_P)
+    return _P(a.data_ptr())  # torch tensor
+
+
+def stream_ptr(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return _P(s.cuda_stream)
+
+
+# ---- thin typed wrappers over the stateless CPU board entry points ----------------------
+
+def _u64(x):
+    return np.ascontiguousarray(x, dtype=np.uint64)
+
+
+def legal_cpu(own, opp):
+    own, opp = _u64(own), _u64(opp)
+    out = np.empty(own.shape, np.uint64)
+    check(lib.oth_legal_cpu(ptr(own), ptr(opp), ptr(out), own.size), "oth_legal_cpu")
+    return out
+
+
+def step_cpu(own, opp, act, raise_illegal=True):
+    own, opp = _u64(own), _u64(opp)
+    act = np.ascontiguousarray(act, dtype=np.uint8)
+    n = own.size
+    o, p, lg = (np.empty(own.shape, np.uint64) for _ in range(3))
+    st = np.empty(own.shape, np.uint16)
+    rc = lib.oth_step_cpu(ptr(own), ptr(opp), ptr(act), ptr(o), ptr(p), ptr(lg), ptr(st), n)
+    if rc != AZ_OK and (raise_illegal or rc != AZ_ERR_ILLEGAL):
+        check(rc, "oth_step_cpu")
+    return o, p, lg, st
+
+
+def make_move_cpu(own, opp, act):
+    own, opp = _u64(own), _u64(opp)
+    act = np.ascontiguousarray(act, dtype=np.uint8)
+    o, p = np.empty(own.shape, np.uint64), np.empty(own.shape, np.uint64)
+    check(lib.oth_make_move_cpu(ptr(own), ptr(opp), ptr(act), ptr(o), ptr(p), own.size),
+          "oth_make_move_cpu")
+    return o, p
+
+
+def pack_np(states, player):
+    states = np.ascontiguousarray(states, dtype=np.int8).reshape(-1, 64)
+    player = np.ascontiguousarray(np.broadcast_to(player, (states.shape[0],)), dtype=np.int8)
+    n = states.shape[0]
+    own, opp = np.empty(n, np.uint64), np.empty(n, np.uint64)
+    check(lib.oth_pack_np(ptr(states), ptr(player), ptr(own), ptr(opp), n), "oth_pack_np")
+    return own, opp
+
+
+def unpack_np(own, opp, player):
+    own, opp = _u64(own).reshape(-1), _u64(opp).reshape(-1)
+    n = own.size
+    player = np.ascontiguousarray(np.broadcast_to(player, (n,)), dtype=np.int8)
+    out = np.empty((n, 64), np.int8)
+    check(lib.oth_unpack_np(ptr(own), ptr(opp), ptr(player), ptr(out), n), "oth_unpack_np")
+    return out.reshape(n, 8, 8)
+
+
+def d4_cpu(x, sym):
+    x = _u64(x)
+    sym = np.ascontiguousarray(np.broadcast_to(sym, x.shape), dtype=np.uint8)
+    out = np.empty(x.shape, np.uint64)
+    check(lib.oth_d4_cpu(ptr(x), ptr(sym), ptr(out), x.size), "oth_d4_cpu")
+    return out
+
+
+def status_flags(st):
+    return np.asarray(st) & 0xFF
+
+
+def status_score(st):
+    return (np.asarray(st) >> 8).astype(np.uint8).view(np.int8).astype(np.int32)

@@ -114,6 +114,22 @@ int oth_step_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   return AZ_OK;
 }
 
+int oth_make_move_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                      uint64_t* own_o, uint64_t* opp_o, int64_t n) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_make_move_cpu: n < 0");
+  AZ_REQUIRE(n == 0 || (own && opp && act && own_o && opp_o), AZ_ERR_ARG,
+             "oth_make_move_cpu: null buffer");
+  for (int64_t i = 0; i < n; ++i) {
+    const int a = act[i];
+    AZ_REQUIRE(a <= 64, AZ_ERR_ARG, "oth_make_move_cpu: action %d out of range", a);
+    // no legality check, exactly like _BitBoard.make_move: an unbounded placement just
+    // adds the stone (captured = 0)
+    const uint64_t cap = a == azb::kPass ? 0ull : azb::flips(own[i], opp[i], a);
+    azb::play(own[i], opp[i], a, cap, own_o + i, opp_o + i);
+  }
+  return AZ_OK;
+}
+
 int oth_pack_np(const int8_t* states, const int8_t* player, uint64_t* own, uint64_t* opp,
                 int64_t n) {
   AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_pack_np: n < 0");

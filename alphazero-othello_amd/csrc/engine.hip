@@ -1,0 +1,1401 @@
+// engine.hip — batched MCTS self-play engine for gfx950.
+//
+// G game slots advance together.  Each slot owns a flat structure-of-arrays node arena
+// (the reference's `Node` objects, MCTS_model.py:46-169, as rows of plain arrays) in two
+// ping-pong halves: the live tree, and the target of the re-root compaction that
+// MCTS.make_move's subtree reuse (MCTS_model.py:200-215) needs.
+//
+// One batched simulation step (graph-capturable, no host synchronisation):
+//   k_select   one wavefront per slot: PUCT descent from the root (MCTS_model.py:362-370,
+//              :129-139, ties -> lowest action), terminal leaves backed up in place
+//              (:381-384); the first unexpanded leaf is packed as the canonical NN input
+//              player*state (Models.py:16) into nn_in[g, 64].
+//   (caller)   policy/value net on nn_in -> priors[g, 65] (softmax), values[g] (tanh).
+//   k_expand   one wavefront per slot: root Dirichlet noise (:340-343), prior masking and
+//              renormalisation (:345-349), eager creation of every legal child — one lane per
+//              square runs that child's board step (flip, next-side legal mask, terminal
+//              check: envs/othello.py:171-200, :157-166, :435-454) — and the sign-alternating
+//              backup (:160-169).
+//   k_move     (auto-play) one workgroup per slot whose search is done: pi from visit
+//              counts (:244-274), trajectory record (self_play_worker.py:72-73), action
+//              sample (:75), the move and terminal check (:77-79), TD(lambda) targets on
+//              game end (:8-35, :80-86) and the re-root compaction (make_move).
+//
+// With one leaf per slot per step the search is exactly the reference with
+// args['num_threads'] = 1: the only virtual loss visible in PUCT is the parent's own (+1 in
+// the sqrt term), which the descent applies directly.  All float arithmetic reproduces the
+// reference's NumPy-2 (NEP 50) promotion; the library is built with -ffp-contract=off.
+#include <math.h>
+
+#include <new>
+#include <vector>
+
+#include "bitboard.h"
+#include "common.h"
+#include "philox.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kSelBlock = 256;  // 4 slots (waves) per workgroup in select / expand
+constexpr int kMoveBlock = 256;
+
+enum : uint8_t { kExpanded = 1, kTerminal = 2, kChildF64 = 4 };
+enum : int32_t { kIdle = AZ_GAME_IDLE, kActive = AZ_GAME_ACTIVE, kFinished = AZ_GAME_FINISHED,
+                 kSearchDone = 3 };
+
+// Node arena: one entry per (half, slot, node).  half in {0,1}, node < cap.
+struct Arena {
+  uint64_t* own;    // side to move at this node
+  uint64_t* opp;
+  uint64_t* legal;  // placements of `own`; 0 => only the pass action (envs/othello.py:401-403)
+  int32_t* N;       // visit_count
+  double* W;        // value_sum (from this node's player's view)
+  double* P;        // prior (f32-exact unless the parent carries kChildF64)
+  int32_t* parent;
+  int32_t* first;   // first child (children contiguous, ascending action)
+  uint8_t* nchild;
+  uint8_t* action;
+  uint8_t* flags;
+  int8_t* tval;     // terminal_value for terminal nodes
+};
+
+struct Games {
+  int32_t* status;
+  int32_t* half;       // live arena half
+  int32_t* n_nodes;
+  int32_t* sims_done;
+  int32_t* sims_target;
+  int32_t* leaf;       // leaf awaiting evaluation, -1 none
+  int32_t* ply;
+  int32_t* root_player;
+  int32_t* winner;
+  int32_t* overflow;
+  int32_t* start_step; // slot becomes active at this engine step (stagger)
+  uint32_t* rng_event; // per-slot RNG event counter
+  uint8_t* sym;        // D4 transform of the pending leaf
+  int32_t* noise_cur;  // injected-stream cursors
+  int32_t* u_cur;
+  // trajectory [G, T]
+  uint64_t* t_own;
+  uint64_t* t_opp;
+  float* t_pi;  // [G, T, 65]
+  int8_t* t_player;
+  double* t_vroot;
+};
+
+struct Counters {  // device-side, 64-bit
+  unsigned long long games_started;
+  unsigned long long games_finished;
+  unsigned long long samples_n;
+  unsigned long long samples_dropped;
+  unsigned long long overflow;
+  unsigned long long step;
+  unsigned long long sims;
+  unsigned long long moves;
+  long long start_budget;  // games still allowed to start (refill)
+  int32_t ready_n;
+  int32_t unlimited;       // refill without a start budget
+};
+
+struct Samples {
+  uint64_t* own;
+  uint64_t* opp;
+  float* pi;  // [cap, 65]
+  double* z;
+  int8_t* player;
+  int32_t* slot;  // game slot that produced the row
+  int64_t cap;
+};
+
+struct Params {
+  Arena a;
+  Games g;
+  Samples s;
+  Counters* ctr;
+  int32_t* ready;  // [G]
+  const double* inj_noise;  // [G, NS, 65]
+  const double* inj_u;      // [G, NU]
+  int32_t G, C, T, NS, NU;
+  int32_t sims;
+  int32_t n_explore;
+  int32_t eval_mode, rng_mode, d4, auto_play, refill;
+  double c_puct, alpha, eps, temp, lambd;
+  uint64_t seed;
+  uint32_t stream_id;
+};
+
+__device__ __forceinline__ int64_t nidx(const Params& p, int half, int g, int i) {
+  return ((int64_t)half * p.G + g) * (int64_t)p.C + i;
+}
+
+// ---------------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+template <typename T>
+__device__ __forceinline__ T shfl(T v, int src) {
+  return __shfl(v, src, kWave);
+}
+
+// NumPy's pairwise sum of a contiguous length-65 vector (numpy/_core/src/umath/
+// loops_utils.h.src pairwise_sum: eight running partials over the first 64 elements,
+// combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail element).  x = this lane's
+// element (lanes 0..63), x64 = element 64.  Returns the sum in every lane.
+template <typename T>
+__device__ T np_sum65(T x, T x64) {
+  const int lane = lane_id();
+  T r = x;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    const T y = shfl(x, (lane + 8 * i) & 63);
+    r = r + y;
+  }
+  const T r0 = shfl(r, 0), r1 = shfl(r, 1), r2 = shfl(r, 2), r3 = shfl(r, 3);
+  const T r4 = shfl(r, 4), r5 = shfl(r, 5), r6 = shfl(r, 6), r7 = shfl(r, 7);
+  T res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  res = res + x64;
+  return res;
+}
+
+__device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
+
+// ---------------------------------------------------------------------------------
+// node helpers (executed by the whole wave; stores by lane 0 only where noted)
+
+__device__ void init_root(const Params& p, int g, int half, uint64_t own, uint64_t opp) {
+  const int64_t r = nidx(p, half, g, 0);
+  p.a.own[r] = own;
+  p.a.opp[r] = opp;
+  p.a.legal[r] = azb::legal(own, opp);
+  p.a.N[r] = 0;
+  p.a.W[r] = 0.0;
+  p.a.P[r] = 0.0;
+  p.a.parent[r] = -1;
+  p.a.first[r] = -1;
+  p.a.nchild[r] = 0;
+  p.a.action[r] = 0;
+  p.a.flags[r] = 0;  // the root is never terminal-flagged (MCTS_model.py:103-106)
+  p.a.tval[r] = 0;
+}
+
+// Node.backpropagate (MCTS_model.py:160-169): N += 1, W += sign*v, sign alternating up.
+__device__ void backup(const Params& p, int g, int half, int node, double v) {
+  double s = 1.0;
+  while (node >= 0) {
+    const int64_t k = nidx(p, half, g, node);
+    p.a.N[k] += 1;
+    p.a.W[k] += s * v;
+    s = -s;
+    node = p.a.parent[k];
+  }
+}
+
+// Pack the canonical NN input player*state (Models.py:16): own stones +1, opponent -1,
+// optionally through D4 transform `sym` (random_symmetry, MCTS_model.py:15-28).
+__device__ void emit_leaf(const Params& p, float* nn_in, int g, uint64_t own, uint64_t opp,
+                          int sym) {
+  const int lane = lane_id();
+  const float v = ((own >> lane) & 1) ? 1.0f : (((opp >> lane) & 1) ? -1.0f : 0.0f);
+  const int dst = sym ? azb::d4_square(lane, sym) : lane;
+  nn_in[(int64_t)g * 64 + dst] = v;
+}
+
+__device__ void emit_none(float* nn_in, int32_t* leaf_o, int g) {
+  nn_in[(int64_t)g * 64 + lane_id()] = 0.0f;
+  if (lane_id() == 0 && leaf_o) leaf_o[g] = -1;
+}
+
+// PUCT child choice of MCTS._select_child / Node._get_ucb_score (MCTS_model.py:129-139,
+// :362-370).  NumPy-2 promotion: with float32 priors every operation after the Python-float
+// sqrt is float32 (c_puct and q are cast to float32); with the Dirichlet-noised root's
+// float64 priors it is all float64.  The node's own virtual visit (+1, MCTS_model.py:378)
+// enters the sqrt; the children carry none.  max() keeps the first maximum in ascending
+// action order, i.e. the lowest child index.
+__device__ int select_child(const Params& p, int g, int half, int node) {
+  const int lane = lane_id();
+  const int64_t k = nidx(p, half, g, node);
+  const int nc = p.a.nchild[k];
+  const int fc = p.a.first[k];
+  const bool f64 = (p.a.flags[k] & kChildF64) != 0;
+  const double sq = sqrt((double)(p.a.N[k] + 1) + 1e-8);
+  double score = -INFINITY;
+  int idx = 0x7fffffff;
+  if (lane < nc) {
+    const int64_t c = nidx(p, half, g, fc + lane);
+    const int n = p.a.N[c];
+    const double w = p.a.W[c];
+    const double pr = p.a.P[c];
+    const double q = -(n == 0 ? 0.0 : w / (double)n);
+    if (f64) {
+      const double u = p.c_puct * pr * sq / (double)(1 + n);
+      score = q + u;
+    } else {
+      const float u = (((float)p.c_puct * (float)pr) * (float)sq) / (float)(1 + n);
+      score = (double)((float)q + u);
+    }
+    idx = lane;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double os = __shfl_xor(score, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    if (os > score || (os == score && oi < idx)) {
+      score = os;
+      idx = oi;
+    }
+  }
+  return fc + idx;
+}
+
+__device__ void push_ready(const Params& p, int g) {
+  const int i = atomicAdd(&p.ctr->ready_n, 1);
+  p.ready[i] = g;
+}
+
+// ---------------------------------------------------------------------------------
+// k_select
+
+__global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restrict__ nn_in,
+                                                      int32_t* __restrict__ leaf_o,
+                                                      int max_descents) {
+  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+  if (g >= p.G) return;
+  const int lane = lane_id();
+  const int status = p.g.status[g];
+  const unsigned long long step = p.ctr->step;
+  if (status != kActive || (long long)step < (long long)p.g.start_step[g]) {
+    emit_none(nn_in, leaf_o, g);
+    return;
+  }
+  const int half = p.g.half[g];
+  int sims_done = p.g.sims_done[g];
+  const int target = p.g.sims_target[g];
+  const int64_t root = nidx(p, half, g, 0);
+  int leaf = -1;
+  if (!(p.a.flags[root] & kExpanded)) {
+    leaf = 0;  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
+  } else {
+    int guard = 0;
+    while (sims_done < target && guard < max_descents) {
+      ++guard;
+      int node = 0;
+      bool done = false;
+      while (!done) {
+        const int64_t k = nidx(p, half, g, node);
+        const uint8_t f = p.a.flags[k];
+        if (f & kTerminal) {  // MCTS_model.py:381-384
+          if (lane == 0) backup(p, g, half, node, (double)p.a.tval[k]);
+          // lane 0's N/W stores must be visible to the wave's next PUCT loads
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          ++sims_done;
+          done = true;
+        } else if (!(f & kExpanded)) {  // MCTS_model.py:386-389
+          leaf = node;
+          done = true;
+        } else {
+          node = select_child(p, g, half, node);
+        }
+      }
+      if (leaf >= 0) break;
+    }
+  }
+  if (leaf >= 0) {
+    const int64_t k = nidx(p, half, g, leaf);
+    int sym = 0;
+    if (p.d4) {
+      const uint32_t ev = p.g.rng_event[g];
+      sym = (int)(azr::uniform1(p.seed, (uint32_t)g, ev, 0x5000u, p.stream_id) * 8.0) & 7;
+      if (lane == 0) {
+        p.g.rng_event[g] = ev + 1;
+        p.g.sym[g] = (uint8_t)sym;
+      }
+    }
+    emit_leaf(p, nn_in, g, p.a.own[k], p.a.opp[k], sym);
+    if (lane == 0) {
+      p.g.leaf[g] = leaf;
+      if (leaf_o) leaf_o[g] = leaf;
+    }
+  } else {
+    emit_none(nn_in, leaf_o, g);
+  }
+  if (lane == 0) {
+    const int prev = p.g.sims_done[g];
+    if (sims_done != prev) {
+      atomicAdd(&p.ctr->sims, (unsigned long long)(sims_done - prev));
+      p.g.sims_done[g] = sims_done;
+    }
+    if (leaf < 0 && sims_done >= target) {
+      if (p.auto_play) push_ready(p, g);
+      else p.g.status[g] = kSearchDone;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// k_expand
+
+// MCTS._rollout (MCTS_model.py:276-303): uniformly random playout; value from the leaf
+// player's view.
+__device__ double rollout(const Params& p, int g, uint64_t own, uint64_t opp) {
+  const uint32_t ev = p.g.rng_event[g];
+  p.g.rng_event[g] = ev + 1;
+  int side = 1;
+  for (uint32_t ply = 0; ply < 256; ++ply) {
+    uint64_t lg = azb::legal(own, opp);
+    int a = azb::kPass;
+    if (lg) {
+      const double u = azr::uniform1(p.seed, (uint32_t)g, ev, 0x6000u + ply, p.stream_id);
+      int j = (int)(u * azb::popc(lg));
+      for (int i = 0; i < j; ++i) lg &= lg - 1;
+      a = __builtin_ctzll(lg);
+    }
+    uint64_t no, np_;
+    azb::play(own, opp, a, a == azb::kPass ? 0ull : azb::flips(own, opp, a), &no, &np_);
+    own = no;
+    opp = np_;
+    side = -side;
+    if (!azb::legal(own, opp) && !azb::legal(opp, own)) {
+      const int d = (azb::popc(own) - azb::popc(opp)) * side;
+      return d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0);
+    }
+  }
+  return 0.0;
+}
+
+__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
+                                                      const float* __restrict__ values) {
+  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+  if (g >= p.G) return;
+  const int lane = lane_id();
+  const int leaf = p.g.leaf[g];
+  if (leaf < 0) return;
+  const int half = p.g.half[g];
+  const int64_t k = nidx(p, half, g, leaf);
+  const uint64_t own = p.a.own[k], opp = p.a.opp[k], lg = p.a.legal[k];
+  const bool is_root = leaf == 0;
+
+  // ---- priors and value (MCTS_model.py:332-337)
+  float pr, pr64;
+  double v;
+  if (p.eval_mode == AZ_EVAL_ROLLOUT) {
+    pr = 1.0f;
+    pr64 = 1.0f;
+    double vv = 0.0;
+    if (lane == 0) vv = rollout(p, g, own, opp);
+    v = shfl(vv, 0);
+  } else {
+    const float* row = priors + (int64_t)g * 65;
+    const int sym = p.d4 ? p.g.sym[g] : 0;
+    // unsymmetrise_pi (MCTS_model.py:31-43): the net saw the board through `sym`
+    pr = row[sym ? azb::d4_square(lane, sym) : lane];
+    pr64 = row[64];
+    v = (double)values[g];
+  }
+  const bool valid = lg ? ((lg >> lane) & 1) != 0 : false;
+  const bool valid64 = lg == 0;
+
+  // ---- noise, mask, renormalise (MCTS_model.py:340-349)
+  const bool noise = is_root && p.eps > 0.0;
+  double P, P64;
+  if (noise) {
+    double n, n64;
+    if (p.rng_mode == AZ_RNG_INJECTED) {
+      const int cur = p.g.noise_cur[g];
+      const double* src = p.inj_noise + ((int64_t)g * p.NS + (cur < p.NS ? cur : p.NS - 1)) * 65;
+      n = src[lane];
+      n64 = src[64];
+      if (lane == 0) p.g.noise_cur[g] = cur + 1;
+    } else {
+      const uint32_t ev = p.g.rng_event[g];
+      const double ga = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, (uint32_t)lane, p.stream_id);
+      const double ga64 = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, 64u, p.stream_id);
+      double s = ga;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+      s += ga64;
+      n = ga / s;
+      n64 = ga64 / s;
+      if (lane == 0) p.g.rng_event[g] = ev + 1;
+    }
+    // (1 - eps) * priors is float32 (Python float x float32 array); + eps * noise is float64
+    const float keep = (float)(1.0 - p.eps);
+    P = (double)(keep * pr) + p.eps * n;
+    P64 = (double)(keep * pr64) + p.eps * n64;
+    P = valid ? P : 0.0 * P;  // priors *= valid_mask
+    P64 = valid64 ? P64 : 0.0 * P64;
+    const double tot = np_sum65<double>(P, P64);
+    if (tot > 1e-12) {
+      P = P / tot;
+      P64 = P64 / tot;
+    }
+  } else {
+    float q = valid ? pr : 0.0f * pr;
+    float q64 = valid64 ? pr64 : 0.0f * pr64;
+    const float tot = np_sum65<float>(q, q64);
+    if (tot > (float)1e-12) {
+      q = q / tot;
+      q64 = q64 / tot;
+    }
+    P = (double)q;
+    P64 = (double)q64;
+  }
+
+  // ---- eager expansion of every legal child (MCTS_model.py:352-357, :146-158)
+  const int nc = lg ? azb::popc(lg) : 1;
+  int fc = 0;
+  if (lane == 0) {
+    fc = p.g.n_nodes[g];
+    if (fc + nc <= p.C) {
+      p.g.n_nodes[g] = fc + nc;
+    } else {
+      fc = -1;
+      p.g.overflow[g] += 1;
+      atomicAdd(&p.ctr->overflow, 1ull);
+    }
+  }
+  fc = shfl(fc, 0);
+  if (fc >= 0) {
+    const bool mine = lg ? valid : (lane == 0);
+    if (mine) {
+      const int a = lg ? lane : azb::kPass;
+      const int ci = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
+      uint64_t co, cp;
+      azb::play(own, opp, a, lg ? azb::flips(own, opp, a) : 0ull, &co, &cp);
+      const uint64_t clg = azb::legal(co, cp);
+      const bool term = clg == 0 && azb::legal(cp, co) == 0;
+      const int d = azb::popc(co) - azb::popc(cp);
+      const int64_t c = nidx(p, half, g, fc + ci);
+      p.a.own[c] = co;
+      p.a.opp[c] = cp;
+      p.a.legal[c] = clg;
+      p.a.N[c] = 0;
+      p.a.W[c] = 0.0;
+      p.a.P[c] = lg ? P : P64;
+      p.a.parent[c] = leaf;
+      p.a.first[c] = -1;
+      p.a.nchild[c] = 0;
+      p.a.action[c] = (uint8_t)a;
+      p.a.flags[c] = term ? kTerminal : 0;
+      p.a.tval[c] = (int8_t)(term ? (d > 0 ? 1 : (d < 0 ? -1 : 0)) : 0);
+    }
+    if (lane == 0) {
+      p.a.first[k] = fc;
+      p.a.nchild[k] = (uint8_t)nc;
+      p.a.flags[k] = p.a.flags[k] | kExpanded | (noise ? kChildF64 : 0);
+    }
+  }
+  if (lane == 0) {
+    backup(p, g, half, leaf, v);  // MCTS_model.py:360
+    p.g.leaf[g] = -1;
+    int sd = p.g.sims_done[g];
+    if (!is_root) {  // the search-start root expansion is not one of the simulations
+      sd += 1;
+      p.g.sims_done[g] = sd;
+      atomicAdd(&p.ctr->sims, 1ull);
+    }
+    if (sd >= p.g.sims_target[g]) {
+      if (p.auto_play) push_ready(p, g);
+      else p.g.status[g] = kSearchDone;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// pi from the root's visit counts (MCTS.policy_improve_step, MCTS_model.py:244-271).
+// Wave-level; lane a holds pi[a] on return, lane 0 additionally *pi64.
+__device__ float root_pi(const Params& p, int g, int half, double temp, double u_tie,
+                         float* pi64) {
+  const int lane = lane_id();
+  const int64_t r = nidx(p, half, g, 0);
+  const int nc = p.a.nchild[r], fc = p.a.first[r];
+  // counts[a] = child visit count (float32), each lane finds the child for its square
+  float c = 0.0f, c64 = 0.0f;
+  if (nc > 0) {
+    // children are sorted by action; lane j reads child j and scatters via shuffles
+    int act = 255;
+    float cnt = 0.0f;
+    if (lane < nc) {
+      const int64_t ck = nidx(p, half, g, fc + lane);
+      act = p.a.action[ck];
+      cnt = (float)p.a.N[ck];
+    }
+    for (int j = 0; j < nc; ++j) {
+      const int aj = shfl(act, j);
+      const float cj = shfl(cnt, j);
+      if (aj == lane) c = cj;
+      if (aj == 64) c64 = cj;
+    }
+  }
+  float pi, p64;
+  if (fabs(temp) < 1e-1) {
+    float m = fmaxf(c, c64);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, kWave));
+    const uint64_t ties = ballot(c == m);
+    const int k = azb::popc(ties) + (c64 == m ? 1 : 0);
+    int j = (int)(u_tie * (double)k);
+    j = j < 0 ? 0 : (j >= k ? k - 1 : j);
+    int best = 64;
+    if (j < azb::popc(ties)) {
+      uint64_t t = ties;
+      for (int i = 0; i < j; ++i) t &= t - 1;
+      best = __builtin_ctzll(t);
+    }
+    const bool any = nc > 0;  // `if len(self.root.valid_actions) != 0`
+    pi = (any && best == lane) ? 1.0f : 0.0f;
+    p64 = (any && best == 64) ? 1.0f : 0.0f;
+  } else {
+    const float ex = (float)(1.0 / temp);
+    const float ce = temp == 1.0 ? c : powf(c, ex);
+    const float ce64 = temp == 1.0 ? c64 : powf(c64, ex);
+    const float norm = np_sum65<float>(ce, ce64);
+    if (norm < (float)1e-12) {
+      // uniform over the root's valid actions (the children)
+      const uint64_t lg = p.a.legal[r];
+      const float u = nc > 0 ? (float)(1.0 / (double)nc) : 0.0f;
+      pi = (lg >> lane) & 1 ? u : 0.0f;
+      p64 = lg == 0 ? u : 0.0f;
+    } else {
+      pi = ce / norm;
+      p64 = ce64 / norm;
+    }
+  }
+  *pi64 = p64;
+  return pi;
+}
+
+// np.random.choice(65, p=pi) given its uniform draw u: cdf = cumsum(float64(pi)) (sequential),
+// cdf /= cdf[-1], searchsorted(u, side='right').  Lane 0 only; the second pass recomputes
+// the same sequential partial sums instead of keeping a 65-entry array in scratch.
+__device__ int sample_action(const float* pis, double u) {
+  double last = 0.0;
+  for (int a = 0; a < 65; ++a) last = last + (double)pis[a];
+  double acc = 0.0;
+  int idx = 0;
+  for (int a = 0; a < 65; ++a) {
+    acc = acc + (double)pis[a];
+    if (acc / last <= u) idx = a + 1;
+  }
+  return idx > 64 ? 64 : idx;
+}
+
+// Re-root compaction: copy the subtree under old node `child` into the other arena half in
+// breadth-first order (children stay contiguous and ascending), making it node 0.  Whole
+// workgroup; map = LDS scratch of p.C ints (new index -> old index).
+__device__ int compact(const Params& p, int g, int child, int32_t* map) {
+  __shared__ int s_scan[kMoveBlock / kWave];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int oh = p.g.half[g], nh = oh ^ 1;
+  if (tid == 0) map[0] = child;
+  __syncthreads();
+  int lo = 0, hi = 1, n_new = 1;
+  while (lo < hi) {
+    for (int s0 = lo; s0 < hi; s0 += kMoveBlock) {
+      const int i = s0 + tid;
+      int old = -1, nc = 0;
+      if (i < hi) {
+        old = map[i];
+        const int64_t ok = nidx(p, oh, g, old);
+        if (p.a.flags[ok] & kExpanded) nc = p.a.nchild[ok];
+      }
+      // block exclusive scan of nc
+      int incl = nc;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) s_scan[wave] = incl;
+      __syncthreads();
+      int wbase = 0, tot = 0;
+      for (int w = 0; w < kMoveBlock / kWave; ++w) {
+        if (w < wave) wbase += s_scan[w];
+        tot += s_scan[w];
+      }
+      const int nfc = n_new + wbase + incl - nc;
+      if (i < hi) {
+        const int64_t ok = nidx(p, oh, g, old);
+        const int64_t nk = nidx(p, nh, g, i);
+        p.a.own[nk] = p.a.own[ok];
+        p.a.opp[nk] = p.a.opp[ok];
+        p.a.legal[nk] = p.a.legal[ok];
+        p.a.N[nk] = p.a.N[ok];
+        p.a.W[nk] = p.a.W[ok];
+        p.a.P[nk] = p.a.P[ok];
+        p.a.action[nk] = p.a.action[ok];
+        p.a.flags[nk] = p.a.flags[ok];
+        p.a.tval[nk] = p.a.tval[ok];
+        p.a.nchild[nk] = (uint8_t)nc;
+        p.a.first[nk] = nc ? nfc : -1;
+        if (i == 0) p.a.parent[nk] = -1;
+        const int ofc = p.a.first[ok];
+        for (int j = 0; j < nc; ++j) {
+          map[nfc + j] = ofc + j;
+          p.a.parent[nidx(p, nh, g, nfc + j)] = i;
+        }
+      }
+      n_new += tot;
+      __syncthreads();
+    }
+    lo = hi;
+    hi = n_new;
+  }
+  if (tid == 0) {
+    p.g.half[g] = nh;
+    p.g.n_nodes[g] = n_new;
+  }
+  __syncthreads();
+  return n_new;
+}
+
+__device__ double next_uniform(const Params& p, int g, uint32_t sub) {
+  if (p.rng_mode == AZ_RNG_INJECTED) {
+    const int cur = p.g.u_cur[g];
+    p.g.u_cur[g] = cur + 1;
+    return cur < p.NU ? p.inj_u[(int64_t)g * p.NU + cur] : 0.5;
+  }
+  const uint32_t ev = p.g.rng_event[g];
+  p.g.rng_event[g] = ev + 1;
+  return azr::uniform1(p.seed, (uint32_t)g, ev, sub, p.stream_id);
+}
+
+__device__ void new_game(const Params& p, int g) {
+  const int half = p.g.half[g];
+  init_root(p, g, half, azb::kInitOwn, azb::kInitOpp);
+  p.g.n_nodes[g] = 1;
+  p.g.ply[g] = 0;
+  p.g.root_player[g] = 1;
+  p.g.winner[g] = 0;
+  p.g.sims_done[g] = 0;
+  p.g.sims_target[g] = p.sims;
+  p.g.leaf[g] = -1;
+  p.g.status[g] = kActive;
+}
+
+// get_training_data (self_play_worker.py:8-35) + append to the sample buffer.
+__device__ void finish_game(const Params& p, int g, int n_plies, int winner) {
+  __shared__ unsigned long long s_base;
+  __shared__ int s_ok;
+  const int tid = threadIdx.x;
+  const int64_t tb = (int64_t)g * p.T;
+  if (tid == 0) {
+    unsigned long long base = atomicAdd(&p.ctr->samples_n, (unsigned long long)n_plies);
+    s_ok = (int64_t)(base + n_plies) <= p.s.cap;
+    if (!s_ok) {
+      atomicAdd(&p.ctr->samples_n, (unsigned long long)(-(long long)n_plies));
+      atomicAdd(&p.ctr->samples_dropped, (unsigned long long)n_plies);
+    }
+    s_base = base;
+    if (s_ok) {
+      double g_next = 0.0;
+      int p_next = 0;
+      for (int t = n_plies - 1; t >= 0; --t) {
+        const int pl = p.g.t_player[tb + t];
+        const double z = winner == 0 ? 0.0 : (pl == winner ? 1.0 : -1.0);
+        double gt;
+        if (t == n_plies - 1) {
+          gt = z;
+        } else {
+          const double sign = pl == p_next ? 1.0 : -1.0;
+          gt = (1.0 - p.lambd) * p.g.t_vroot[tb + t] + p.lambd * sign * g_next;
+        }
+        p.s.z[base + t] = gt;
+        g_next = gt;
+        p_next = pl;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_ok) {
+    const unsigned long long base = s_base;
+    for (int t = tid; t < n_plies; t += blockDim.x) {
+      p.s.own[base + t] = p.g.t_own[tb + t];
+      p.s.opp[base + t] = p.g.t_opp[tb + t];
+      p.s.player[base + t] = p.g.t_player[tb + t];
+      p.s.slot[base + t] = g;
+    }
+    for (int e = tid; e < n_plies * 65; e += blockDim.x)
+      p.s.pi[base * 65 + e] = p.g.t_pi[tb * 65 + e];
+  }
+  __syncthreads();
+}
+
+// k_move: one workgroup per slot in the ready list.
+__global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
+  extern __shared__ int32_t map[];
+  __shared__ float s_pi[65];
+  __shared__ int s_child, s_term, s_winner, s_restart;
+  const int tid = threadIdx.x;
+  const int n_ready = p.ctr->ready_n;
+  for (int ri = blockIdx.x; ri < n_ready; ri += gridDim.x) {
+    const int g = p.ready[ri];
+    const int half = p.g.half[g];
+    const int ply = p.g.ply[g];
+    const int player = p.g.root_player[g];
+    if (tid < 64) {
+      // ---- pi (MCTS_model.py:244-271) and trajectory record (self_play_worker.py:72-73)
+      const double temp = ply < p.n_explore ? p.temp : 0.0;
+      double u_tie = 0.0;
+      if (fabs(temp) < 1e-1) {
+        double u = 0.0;
+        if (tid == 0) u = next_uniform(p, g, 0x1000u);
+        u_tie = shfl(u, 0);
+      }
+      float p64;
+      const float pi = root_pi(p, g, half, temp, u_tie, &p64);
+      s_pi[tid] = pi;
+      if (tid == 0) s_pi[64] = p64;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      const int64_t r = nidx(p, half, g, 0);
+      const bool room = ply < p.T;
+      if (room) p.g.t_pi[((int64_t)g * p.T + ply) * 65 + tid] = pi;
+      if (tid == 0) {
+        if (room) {
+          p.g.t_pi[((int64_t)g * p.T + ply) * 65 + 64] = p64;
+          p.g.t_own[(int64_t)g * p.T + ply] = p.a.own[r];
+          p.g.t_opp[(int64_t)g * p.T + ply] = p.a.opp[r];
+          p.g.t_player[(int64_t)g * p.T + ply] = (int8_t)player;
+          const int n = p.a.N[r];
+          p.g.t_vroot[(int64_t)g * p.T + ply] = n == 0 ? 0.0 : p.a.W[r] / (double)n;
+        }
+        // ---- action sample (self_play_worker.py:75)
+        const double u = next_uniform(p, g, 0x2000u);
+        const int a = sample_action(s_pi, u);
+        // ---- the move: re-root to that child (MCTS.make_move, MCTS_model.py:200-215)
+        const int nc = p.a.nchild[r], fc = p.a.first[r];
+        int child = -1;
+        for (int j = 0; j < nc; ++j)
+          if (p.a.action[nidx(p, half, g, fc + j)] == a) child = fc + j;
+        s_child = child;
+        int term = 1, winner = 0;
+        if (child >= 0) {
+          const int64_t ck = nidx(p, half, g, child);
+          // get_value_and_terminated from the mover's view (self_play_worker.py:77-86)
+          term = (p.a.flags[ck] & kTerminal) ? 1 : 0;
+          const int d = azb::popc(p.a.opp[ck]) - azb::popc(p.a.own[ck]);
+          winner = d > 0 ? player : (d < 0 ? -player : 0);
+        }
+        if (!room) term = 1;  // trajectory capacity exhausted (never at T >= 128)
+        s_term = term;
+        s_winner = winner;
+        atomicAdd(&p.ctr->moves, 1ull);
+      }
+    }
+    __syncthreads();
+    if (s_term) {
+      const int n_plies = ply + 1 < p.T ? ply + 1 : p.T;
+      finish_game(p, g, n_plies, s_winner);
+      if (tid == 0) {
+        p.g.winner[g] = s_winner;
+        atomicAdd(&p.ctr->games_finished, 1ull);
+        int restart = 0;
+        if (p.refill) {
+          if (p.ctr->unlimited) {
+            restart = 1;
+          } else {
+            unsigned long long* b = (unsigned long long*)&p.ctr->start_budget;
+            const long long prev = (long long)atomicAdd(b, (unsigned long long)(-1ll));
+            if (prev > 0) restart = 1;
+            else atomicAdd(b, 1ull);
+          }
+        }
+        s_restart = restart;
+        if (restart) {
+          atomicAdd(&p.ctr->games_started, 1ull);
+          p.g.status[g] = kActive;
+        } else {
+          p.g.status[g] = kFinished;
+        }
+      }
+      __syncthreads();
+      if (s_restart && tid == 0) new_game(p, g);
+    } else {
+      compact(p, g, s_child, map);
+      if (tid == 0) {
+        p.g.ply[g] = ply + 1;
+        p.g.root_player[g] = -player;
+        p.g.sims_done[g] = 0;
+        p.g.sims_target[g] = p.sims;
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0) {
+    p.ctr->step += 1;
+  }
+}
+
+// step counter for engines without auto-play (k_move not launched)
+__global__ void k_tick(Counters* c) { c->step += 1; }
+
+// ---------------------------------------------------------------------------------
+// host-driven (MCTS API) kernels
+
+__global__ void k_reset(Params p, long long budget, int stagger) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) {
+    p.ctr->games_started = 0;
+    p.ctr->games_finished = 0;
+    p.ctr->samples_n = 0;
+    p.ctr->samples_dropped = 0;
+    p.ctr->overflow = 0;
+    p.ctr->step = 0;
+    p.ctr->sims = 0;
+    p.ctr->moves = 0;
+    p.ctr->ready_n = 0;
+  }
+  if (g >= p.G) return;
+  p.g.half[g] = 0;
+  p.g.overflow[g] = 0;
+  p.g.rng_event[g] = 0;
+  p.g.noise_cur[g] = 0;
+  p.g.u_cur[g] = 0;
+  p.g.sym[g] = 0;
+  p.g.start_step[g] = stagger > 0 ? (int)((long long)g * stagger / p.G) : 0;
+  new_game(p, g);
+  if (budget >= 0 && g >= budget) p.g.status[g] = kIdle;
+  if (g == 0) {
+    const long long started = budget < 0 ? p.G : (budget < p.G ? budget : p.G);
+    p.ctr->games_started = (unsigned long long)started;
+    p.ctr->start_budget = budget < 0 ? 0 : budget - started;
+    p.ctr->unlimited = budget < 0 ? 1 : 0;
+  }
+}
+
+__global__ void k_set_root(Params p, int g, uint64_t own, uint64_t opp, int player) {
+  if (threadIdx.x != 0) return;
+  p.g.half[g] = 0;
+  init_root(p, g, 0, own, opp);
+  p.g.n_nodes[g] = 1;
+  p.g.root_player[g] = player;
+  p.g.leaf[g] = -1;
+  p.g.sims_done[g] = 0;
+  p.g.sims_target[g] = 0;
+  p.g.status[g] = kSearchDone;
+}
+
+__global__ void k_begin(Params p, int slot, int sims) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= p.G || (slot >= 0 && g != slot)) return;
+  if (p.g.status[g] == kIdle || p.g.status[g] == kFinished) return;
+  p.g.sims_done[g] = 0;
+  p.g.sims_target[g] = sims;
+  p.g.leaf[g] = -1;
+  p.g.status[g] = kActive;
+}
+
+__global__ void k_policy(Params p, int slot, double temp, double u_tie, float* pi_o,
+                         double* vroot_o, int32_t* counts_o) {
+  const int g = slot;
+  const int lane = threadIdx.x;
+  const int half = p.g.half[g];
+  float p64;
+  const float pi = root_pi(p, g, half, temp, u_tie, &p64);
+  pi_o[lane] = pi;
+  if (lane == 0) pi_o[64] = p64;
+  const int64_t r = nidx(p, half, g, 0);
+  if (counts_o) {
+    counts_o[lane] = 0;
+    if (lane == 0) counts_o[64] = 0;
+  }
+  if (lane == 0) {
+    const int n = p.a.N[r];
+    *vroot_o = n == 0 ? 0.0 : p.a.W[r] / (double)n;
+    if (counts_o) {
+      const int nc = p.a.nchild[r], fc = p.a.first[r];
+      for (int j = 0; j < nc; ++j) {
+        const int64_t c = nidx(p, half, g, fc + j);
+        counts_o[p.a.action[c]] = p.a.N[c];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMoveBlock) void k_reroot(Params p, int g, int action,
+                                                       int32_t* result) {
+  extern __shared__ int32_t map[];
+  __shared__ int s_child;
+  const int half = p.g.half[g];
+  if (threadIdx.x == 0) {
+    const int64_t r = nidx(p, half, g, 0);
+    const int nc = (p.a.flags[r] & kExpanded) ? p.a.nchild[r] : 0, fc = p.a.first[r];
+    int child = -1;
+    for (int j = 0; j < nc; ++j)
+      if (p.a.action[nidx(p, half, g, fc + j)] == action) child = fc + j;
+    s_child = child;
+    *result = child;
+  }
+  __syncthreads();
+  if (s_child < 0) return;
+  const int player = p.g.root_player[g];
+  compact(p, g, s_child, map);
+  if (threadIdx.x == 0) {
+    p.g.root_player[g] = -player;
+    p.g.sims_done[g] = 0;
+    p.g.sims_target[g] = 0;
+    p.g.status[g] = kSearchDone;
+  }
+}
+
+}  // namespace
+
+// ====================================================================================
+// host side
+
+struct az_engine {
+  az_config cfg;
+  Params p;
+  std::vector<void*> allocs;
+  int32_t* d_result = nullptr;
+  char* d_scratch = nullptr;  // 1 KiB: az_root_policy outputs
+  size_t lds_move = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(az_engine* e, T** ptr, size_t count) {
+  void* q = nullptr;
+  const size_t bytes = count * sizeof(T) > 0 ? count * sizeof(T) : 16;
+  hipError_t err = hipMalloc(&q, bytes);
+  if (err != hipSuccess)
+    return azc::set_error(AZ_ERR_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(err));
+  e->allocs.push_back(q);
+  *ptr = static_cast<T*>(q);
+  return AZ_OK;
+}
+
+#define AZ_TRY(x)            \
+  do {                       \
+    int rc_ = (x);           \
+    if (rc_ != AZ_OK) return rc_; \
+  } while (0)
+
+void free_all(az_engine* e) {
+  for (void* q : e->allocs) (void)hipFree(q);
+  e->allocs.clear();
+}
+
+unsigned sel_grid(const az_engine* e) {
+  const int per = kSelBlock / kWave;
+  return (unsigned)((e->p.G + per - 1) / per);
+}
+
+}  // namespace
+
+extern "C" {
+
+int az_engine_create(const az_config* cfg_in, az_engine** out) {
+  AZ_GUARD_BEGIN
+  AZ_REQUIRE(cfg_in && out, AZ_ERR_ARG, "az_engine_create: null argument");
+  az_config cfg = *cfg_in;
+  if (cfg.node_capacity <= 0) cfg.node_capacity = 16384;
+  if (cfg.max_plies <= 0) cfg.max_plies = 128;
+  AZ_REQUIRE(cfg.n_games > 0, AZ_ERR_ARG, "n_games must be > 0");
+  AZ_REQUIRE(cfg.node_capacity >= 128 && cfg.node_capacity <= 32768, AZ_ERR_ARG,
+             "node_capacity must be in [128, 32768] (LDS re-root scratch), got %d",
+             cfg.node_capacity);
+  AZ_REQUIRE(cfg.num_simulations >= 0, AZ_ERR_ARG, "num_simulations must be >= 0");
+  AZ_REQUIRE(cfg.eval_mode == AZ_EVAL_EXTERNAL || cfg.eval_mode == AZ_EVAL_ROLLOUT, AZ_ERR_ARG,
+             "bad eval_mode");
+  AZ_REQUIRE(cfg.rng_mode == AZ_RNG_DEVICE || cfg.rng_mode == AZ_RNG_INJECTED, AZ_ERR_ARG,
+             "bad rng_mode");
+  if (cfg.sample_capacity <= 0) cfg.sample_capacity = (int64_t)cfg.n_games * cfg.max_plies * 2;
+  if (cfg.inj_noise_slots <= 0) cfg.inj_noise_slots = 1;
+  if (cfg.inj_uniform_slots <= 0) cfg.inj_uniform_slots = 1;
+
+  az_engine* e = new (std::nothrow) az_engine();
+  AZ_REQUIRE(e, AZ_ERR_ARG, "out of host memory");
+  e->cfg = cfg;
+  Params& p = e->p;
+  p.G = cfg.n_games;
+  p.C = cfg.node_capacity;
+  p.T = cfg.max_plies;
+  p.NS = cfg.inj_noise_slots;
+  p.NU = cfg.inj_uniform_slots;
+  p.sims = cfg.num_simulations;
+  p.n_explore = cfg.num_exploratory_moves;
+  p.eval_mode = cfg.eval_mode;
+  p.rng_mode = cfg.rng_mode;
+  p.d4 = cfg.d4_augment ? 1 : 0;
+  p.auto_play = cfg.auto_play ? 1 : 0;
+  p.refill = cfg.refill ? 1 : 0;
+  p.c_puct = cfg.c_puct;
+  p.alpha = cfg.dirichlet_alpha;
+  p.eps = cfg.dirichlet_epsilon;
+  p.temp = cfg.temperature;
+  p.lambd = cfg.lambd;
+  p.seed = cfg.seed;
+  p.stream_id = (uint32_t)cfg.stream_id;
+
+  const size_t nodes = (size_t)2 * p.G * p.C;
+  const size_t G = p.G, T = p.T;
+  int rc = AZ_OK;
+  auto chk = [&](int r) {
+    if (rc == AZ_OK) rc = r;
+  };
+  chk(dalloc(e, &p.a.own, nodes));
+  chk(dalloc(e, &p.a.opp, nodes));
+  chk(dalloc(e, &p.a.legal, nodes));
+  chk(dalloc(e, &p.a.N, nodes));
+  chk(dalloc(e, &p.a.W, nodes));
+  chk(dalloc(e, &p.a.P, nodes));
+  chk(dalloc(e, &p.a.parent, nodes));
+  chk(dalloc(e, &p.a.first, nodes));
+  chk(dalloc(e, &p.a.nchild, nodes));
+  chk(dalloc(e, &p.a.action, nodes));
+  chk(dalloc(e, &p.a.flags, nodes));
+  chk(dalloc(e, &p.a.tval, nodes));
+  chk(dalloc(e, &p.g.status, G));
+  chk(dalloc(e, &p.g.half, G));
+  chk(dalloc(e, &p.g.n_nodes, G));
+  chk(dalloc(e, &p.g.sims_done, G));
+  chk(dalloc(e, &p.g.sims_target, G));
+  chk(dalloc(e, &p.g.leaf, G));
+  chk(dalloc(e, &p.g.ply, G));
+  chk(dalloc(e, &p.g.root_player, G));
+  chk(dalloc(e, &p.g.winner, G));
+  chk(dalloc(e, &p.g.overflow, G));
+  chk(dalloc(e, &p.g.start_step, G));
+  chk(dalloc(e, &p.g.rng_event, G));
+  chk(dalloc(e, &p.g.sym, G));
+  chk(dalloc(e, &p.g.noise_cur, G));
+  chk(dalloc(e, &p.g.u_cur, G));
+  chk(dalloc(e, &p.g.t_own, G * T));
+  chk(dalloc(e, &p.g.t_opp, G * T));
+  chk(dalloc(e, &p.g.t_pi, G * T * 65));
+  chk(dalloc(e, &p.g.t_player, G * T));
+  chk(dalloc(e, &p.g.t_vroot, G * T));
+  p.s.cap = cfg.sample_capacity;
+  chk(dalloc(e, &p.s.own, (size_t)p.s.cap));
+  chk(dalloc(e, &p.s.opp, (size_t)p.s.cap));
+  chk(dalloc(e, &p.s.pi, (size_t)p.s.cap * 65));
+  chk(dalloc(e, &p.s.z, (size_t)p.s.cap));
+  chk(dalloc(e, &p.s.player, (size_t)p.s.cap));
+  chk(dalloc(e, &p.s.slot, (size_t)p.s.cap));
+  chk(dalloc(e, &p.ctr, 1));
+  chk(dalloc(e, &p.ready, G));
+  double* noise = nullptr;
+  double* uni = nullptr;
+  if (cfg.rng_mode == AZ_RNG_INJECTED) {
+    chk(dalloc(e, &noise, G * p.NS * 65));
+    chk(dalloc(e, &uni, G * p.NU));
+  }
+  p.inj_noise = noise;
+  p.inj_u = uni;
+  chk(dalloc(e, &e->d_result, 4));
+  chk(dalloc(e, &e->d_scratch, 1024));
+  if (rc != AZ_OK) {
+    free_all(e);
+    delete e;
+    return rc;
+  }
+  e->lds_move = (size_t)p.C * sizeof(int32_t);
+  if (hipFuncSetAttribute((const void*)k_move, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_reroot, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess) {
+    (void)hipGetLastError();
+  }
+  if (hipMemset(p.ctr, 0, sizeof(Counters)) != hipSuccess ||
+      hipMemset(p.g.status, 0, G * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(p.g.leaf, 0xff, G * sizeof(int32_t)) != hipSuccess) {
+    free_all(e);
+    delete e;
+    return azc::set_error(AZ_ERR_HIP, "hipMemset failed");
+  }
+  *out = e;
+  return AZ_OK;
+  AZ_GUARD_END
+}
+
+int az_engine_destroy(az_engine* e) {
+  if (!e) return AZ_OK;
+  (void)hipDeviceSynchronize();
+  free_all(e);
+  delete e;
+  return AZ_OK;
+}
+
+int az_reset_all(az_engine* e, int64_t start_budget, int32_t stagger_steps, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  hipStream_t s = azc::as_stream(stream);
+  const unsigned grid = (unsigned)((e->p.G + 255) / 256);
+  hipLaunchKernelGGL(k_reset, dim3(grid), dim3(256), 0, s, e->p, (long long)start_budget,
+                     (int)stagger_steps);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_set_root(az_engine* e, int32_t slot, uint64_t own, uint64_t opp, int32_t player,
+                void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot %d out of range", slot);
+  AZ_REQUIRE((own & opp) == 0, AZ_ERR_ARG, "own and opp overlap");
+  AZ_REQUIRE(player == 1 || player == -1, AZ_ERR_ARG, "player must be +1 or -1");
+  hipStream_t s = azc::as_stream(stream);
+  hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, s, e->p, (int)slot, own, opp,
+                     (int)player);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_begin_search(az_engine* e, int32_t slot, int32_t num_simulations, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(slot >= -1 && slot < e->p.G, AZ_ERR_ARG, "slot %d out of range", slot);
+  AZ_REQUIRE(num_simulations >= 0, AZ_ERR_ARG, "num_simulations < 0");
+  hipStream_t s = azc::as_stream(stream);
+  const unsigned grid = (unsigned)((e->p.G + 255) / 256);
+  hipLaunchKernelGGL(k_begin, dim3(grid), dim3(256), 0, s, e->p, (int)slot,
+                     (int)num_simulations);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
+  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select: null argument");
+  hipStream_t s = azc::as_stream(stream);
+  AZ_HIP(hipMemsetAsync(&e->p.ctr->ready_n, 0, sizeof(int32_t), s));
+  const int max_descents = 4 * (e->p.sims + 1) + 64;
+  hipLaunchKernelGGL(k_select, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in, leaf_o,
+                     max_descents);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int az_expand_backup(az_engine* e, const float* priors, const float* values, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
+             "az_expand_backup: priors/values required in external-eval mode");
+  hipStream_t s = azc::as_stream(stream);
+  hipLaunchKernelGGL(k_expand, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors, values);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int az_play(az_engine* e, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  hipStream_t s = azc::as_stream(stream);
+  if (!e->p.auto_play) {
+    hipLaunchKernelGGL(k_tick, dim3(1), dim3(1), 0, s, e->p.ctr);
+    AZ_HIP(hipGetLastError());
+    return AZ_OK;
+  }
+  const int blocks = e->p.G < 256 ? e->p.G : 256;
+  hipLaunchKernelGGL(k_move, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->p);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int az_inject(az_engine* e, const double* noise, const double* uniforms, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(e->p.rng_mode == AZ_RNG_INJECTED, AZ_ERR_STATE, "engine not in injected-RNG mode");
+  hipStream_t s = azc::as_stream(stream);
+  const size_t G = e->p.G;
+  if (noise)
+    AZ_HIP(hipMemcpyAsync((void*)e->p.inj_noise, noise, G * e->p.NS * 65 * sizeof(double),
+                          hipMemcpyHostToDevice, s));
+  if (uniforms)
+    AZ_HIP(hipMemcpyAsync((void*)e->p.inj_u, uniforms, G * e->p.NU * sizeof(double),
+                          hipMemcpyHostToDevice, s));
+  AZ_HIP(hipMemsetAsync(e->p.g.noise_cur, 0, G * sizeof(int32_t), s));
+  AZ_HIP(hipMemsetAsync(e->p.g.u_cur, 0, G * sizeof(int32_t), s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_root_policy(az_engine* e, int32_t slot, double temp, double u_tie, float* pi_o,
+                   int32_t* counts_o, double* vroot_o, void* stream) {
+  AZ_REQUIRE(e && pi_o, AZ_ERR_ARG, "az_root_policy: null argument");
+  AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot out of range");
+  hipStream_t s = azc::as_stream(stream);
+  float* d_pi = (float*)e->d_scratch;                  // [0, 260)
+  double* d_v = (double*)(e->d_scratch + 264);          // [264, 272)
+  int32_t* d_c = (int32_t*)(e->d_scratch + 272);        // [272, 532)
+  hipLaunchKernelGGL(k_policy, dim3(1), dim3(64), 0, s, e->p, (int)slot, temp, u_tie, d_pi, d_v,
+                     d_c);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipMemcpyAsync(pi_o, d_pi, 65 * sizeof(float), hipMemcpyDeviceToHost, s));
+  double v = 0.0;
+  int32_t c[65];
+  AZ_HIP(hipMemcpyAsync(&v, d_v, sizeof(double), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipMemcpyAsync(c, d_c, sizeof(c), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  if (vroot_o) *vroot_o = v;
+  if (counts_o)
+    for (int i = 0; i < 65; ++i) counts_o[i] = c[i];
+  return AZ_OK;
+}
+
+int az_make_move(az_engine* e, int32_t slot, int32_t action, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot out of range");
+  AZ_REQUIRE(action >= 0 && action <= 64, AZ_ERR_STATE, "%d", action);
+  hipStream_t s = azc::as_stream(stream);
+  hipLaunchKernelGGL(k_reroot, dim3(1), dim3(kMoveBlock), e->lds_move, s, e->p, (int)slot,
+                     (int)action, e->d_result);
+  AZ_HIP(hipGetLastError());
+  int32_t child = -1;
+  AZ_HIP(hipMemcpyAsync(&child, e->d_result, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  // KeyError in the reference (MCTS_model.py:214)
+  AZ_REQUIRE(child >= 0, AZ_ERR_STATE, "%d", action);
+  return AZ_OK;
+}
+
+int az_counters(az_engine* e, int64_t* out8, void* stream) {
+  AZ_REQUIRE(e && out8, AZ_ERR_ARG, "null argument");
+  hipStream_t s = azc::as_stream(stream);
+  Counters c;
+  AZ_HIP(hipMemcpyAsync(&c, e->p.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  out8[0] = (int64_t)c.games_started;
+  out8[1] = (int64_t)c.games_finished;
+  out8[2] = (int64_t)c.samples_n;
+  out8[3] = (int64_t)c.samples_dropped;
+  out8[4] = (int64_t)c.overflow;
+  out8[5] = (int64_t)c.step;
+  out8[6] = (int64_t)c.sims;
+  out8[7] = (int64_t)c.moves;
+  return AZ_OK;
+}
+
+int az_game_info(az_engine* e, int32_t* status, int32_t* ply, int32_t* winner,
+                 int32_t* root_player, int32_t* n_nodes, int32_t* overflow, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  hipStream_t s = azc::as_stream(stream);
+  const size_t b = (size_t)e->p.G * sizeof(int32_t);
+  if (status) AZ_HIP(hipMemcpyAsync(status, e->p.g.status, b, hipMemcpyDeviceToHost, s));
+  if (ply) AZ_HIP(hipMemcpyAsync(ply, e->p.g.ply, b, hipMemcpyDeviceToHost, s));
+  if (winner) AZ_HIP(hipMemcpyAsync(winner, e->p.g.winner, b, hipMemcpyDeviceToHost, s));
+  if (root_player)
+    AZ_HIP(hipMemcpyAsync(root_player, e->p.g.root_player, b, hipMemcpyDeviceToHost, s));
+  if (n_nodes) AZ_HIP(hipMemcpyAsync(n_nodes, e->p.g.n_nodes, b, hipMemcpyDeviceToHost, s));
+  if (overflow) AZ_HIP(hipMemcpyAsync(overflow, e->p.g.overflow, b, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_export_tree(az_engine* e, int32_t slot, int32_t max_nodes, uint64_t* own, uint64_t* opp,
+                   uint64_t* legal, int32_t* N, double* W, double* prior, int32_t* parent,
+                   int32_t* first_child, uint8_t* nchild, uint8_t* action, uint8_t* flags,
+                   int8_t* tval, int32_t* n_nodes_o, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot out of range");
+  hipStream_t s = azc::as_stream(stream);
+  int32_t half = 0, n = 0;
+  AZ_HIP(hipMemcpyAsync(&half, e->p.g.half + slot, 4, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipMemcpyAsync(&n, e->p.g.n_nodes + slot, 4, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  if (n_nodes_o) *n_nodes_o = n;
+  const int m = n < max_nodes ? n : max_nodes;
+  if (m <= 0) return AZ_OK;
+  const int64_t off = ((int64_t)half * e->p.G + slot) * e->p.C;
+#define CP(dst, src, T)                                                                   \
+  if (dst) AZ_HIP(hipMemcpyAsync(dst, e->p.a.src + off, (size_t)m * sizeof(T),             \
+                                 hipMemcpyDeviceToHost, s));
+  CP(own, own, uint64_t)
+  CP(opp, opp, uint64_t)
+  CP(legal, legal, uint64_t)
+  CP(N, N, int32_t)
+  CP(W, W, double)
+  CP(prior, P, double)
+  CP(parent, parent, int32_t)
+  CP(first_child, first, int32_t)
+  CP(nchild, nchild, uint8_t)
+  CP(action, action, uint8_t)
+  CP(flags, flags, uint8_t)
+  CP(tval, tval, int8_t)
+#undef CP
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_export_trajectory(az_engine* e, int32_t slot, int32_t max_plies, uint64_t* own,
+                         uint64_t* opp, float* pi, int8_t* player, double* vroot,
+                         int32_t* n_plies_o, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot out of range");
+  hipStream_t s = azc::as_stream(stream);
+  int32_t ply = 0, st = 0;
+  AZ_HIP(hipMemcpyAsync(&ply, e->p.g.ply + slot, 4, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipMemcpyAsync(&st, e->p.g.status + slot, 4, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  int n = st == kFinished ? ply + 1 : ply;
+  if (n > e->p.T) n = e->p.T;
+  if (n_plies_o) *n_plies_o = n;
+  const int m = n < max_plies ? n : max_plies;
+  if (m <= 0) return AZ_OK;
+  const int64_t off = (int64_t)slot * e->p.T;
+  if (own) AZ_HIP(hipMemcpyAsync(own, e->p.g.t_own + off, m * 8, hipMemcpyDeviceToHost, s));
+  if (opp) AZ_HIP(hipMemcpyAsync(opp, e->p.g.t_opp + off, m * 8, hipMemcpyDeviceToHost, s));
+  if (pi)
+    AZ_HIP(hipMemcpyAsync(pi, e->p.g.t_pi + off * 65, (size_t)m * 65 * 4, hipMemcpyDeviceToHost, s));
+  if (player)
+    AZ_HIP(hipMemcpyAsync(player, e->p.g.t_player + off, m, hipMemcpyDeviceToHost, s));
+  if (vroot)
+    AZ_HIP(hipMemcpyAsync(vroot, e->p.g.t_vroot + off, m * 8, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_samples(az_engine* e, uint64_t** own, uint64_t** opp, float** pi, double** z,
+               int8_t** player, int64_t* n, int64_t* capacity) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  if (own) *own = e->p.s.own;
+  if (opp) *opp = e->p.s.opp;
+  if (pi) *pi = e->p.s.pi;
+  if (z) *z = e->p.s.z;
+  if (player) *player = e->p.s.player;
+  if (capacity) *capacity = e->p.s.cap;
+  if (n) {
+    Counters c;
+    AZ_HIP(hipMemcpy(&c, e->p.ctr, sizeof(Counters), hipMemcpyDeviceToHost));
+    *n = (int64_t)c.samples_n;
+  }
+  return AZ_OK;
+}
+
+int az_copy_samples(az_engine* e, int64_t start, int64_t n, uint64_t* own, uint64_t* opp,
+                    float* pi, double* z, int8_t* player, int32_t* slot, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(start >= 0 && n >= 0 && start + n <= e->p.s.cap, AZ_ERR_ARG,
+             "sample range [%lld, %lld) outside capacity %lld", (long long)start,
+             (long long)(start + n), (long long)e->p.s.cap);
+  if (n == 0) return AZ_OK;
+  hipStream_t s = azc::as_stream(stream);
+  const auto k = hipMemcpyDefault;  // host or device destinations (unified addressing)
+  if (own) AZ_HIP(hipMemcpyAsync(own, e->p.s.own + start, n * 8, k, s));
+  if (opp) AZ_HIP(hipMemcpyAsync(opp, e->p.s.opp + start, n * 8, k, s));
+  if (pi) AZ_HIP(hipMemcpyAsync(pi, e->p.s.pi + start * 65, n * 65 * 4, k, s));
+  if (z) AZ_HIP(hipMemcpyAsync(z, e->p.s.z + start, n * 8, k, s));
+  if (player) AZ_HIP(hipMemcpyAsync(player, e->p.s.player + start, n, k, s));
+  if (slot) AZ_HIP(hipMemcpyAsync(slot, e->p.s.slot + start, n * 4, k, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_clear_samples(az_engine* e, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  hipStream_t s = azc::as_stream(stream);
+  AZ_HIP(hipMemsetAsync(&e->p.ctr->samples_n, 0, sizeof(unsigned long long), s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_engine_geometry(az_engine* e, int32_t* n_games, int32_t* node_capacity,
+                       int32_t* max_plies) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  if (n_games) *n_games = e->p.G;
+  if (node_capacity) *node_capacity = e->p.C;
+  if (max_plies) *max_plies = e->p.T;
+  return AZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+"""Batched GPU self-play: the owner of an `az_engine` handle (include/az_othello.h) and the
+driver loop that replaces the reference's process-pool of `one_self_play` calls
+(train.py:199-225, self_play_worker.py:38-88).
+
+Per simulation step (all on one HIP stream, no host synchronisation, optionally one
+captured HIP graph):
+
+    az_select         leaves of every active game -> canonical planes nn_in [G, 64]
+    net               PyTorch-ROCm forward on nn_in -> softmax priors [G, 65], values [G]
+    az_expand_backup  eager expansion + backup
+    az_play           games whose search finished: pi, record, sample, move, TD(lambda)
+                      targets on game end, re-root; finished slots restart
+
+The host only reads counters.  Finished games' samples accumulate in a device buffer in
+the reference's training-tuple layout (canonical state, pi, target).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+import az_native as nat
+
+SAMPLE_FIELDS = ("own", "opp", "pi", "z", "player", "slot")
+
+
+class Engine:
+    """RAII owner of one az_engine handle plus its per-step device buffers."""
+
+    def __init__(self, n_games, num_simulations, c_puct=2.0, dirichlet_alpha=1.0,
+                 dirichlet_epsilon=0.0, temperature=1.0, num_exploratory_moves=0,
+                 lambd=1.0, rollout=False, injected_rng=False, d4_augment=False,
+                 auto_play=True, refill=False, node_capacity=0, max_plies=0,
+                 sample_capacity=0, inj_noise_slots=1, inj_uniform_slots=1, seed=0,
+                 stream_id=0, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("the self-play engine needs a HIP device (no CPU fallback)")
+        self.device = torch.device(device if device is not None else "cuda")
+        cfg = nat.AzConfig()
+        cfg.n_games = int(n_games)
+        cfg.node_capacity = int(node_capacity)
+        cfg.max_plies = int(max_plies)
+        cfg.num_simulations = int(num_simulations)
+        cfg.c_puct = float(c_puct)
+        cfg.dirichlet_alpha = float(dirichlet_alpha)
+        cfg.dirichlet_epsilon = float(dirichlet_epsilon)
+        cfg.temperature = float(temperature)
+        cfg.num_exploratory_moves = int(num_exploratory_moves)
+        cfg.lambd = float(lambd)
+        cfg.eval_mode = nat.AZ_EVAL_ROLLOUT if rollout else nat.AZ_EVAL_EXTERNAL
+        cfg.rng_mode = nat.AZ_RNG_INJECTED if injected_rng else nat.AZ_RNG_DEVICE
+        cfg.d4_augment = int(bool(d4_augment))
+        cfg.auto_play = int(bool(auto_play))
+        cfg.refill = int(bool(refill))
+        cfg.sample_capacity = int(sample_capacity)
+        cfg.inj_noise_slots = int(inj_noise_slots)
+        cfg.inj_uniform_slots = int(inj_uniform_slots)
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.stream_id = int(stream_id)
+        self.cfg = cfg
+        self.rollout = rollout
+        with torch.cuda.device(self.device):
+            h = ctypes.c_void_p()
+            nat.check(nat.lib.az_engine_create(ctypes.byref(cfg), ctypes.byref(h)),
+                      "az_engine_create")
+            self.h = h
+            G, C, T = (ctypes.c_int32() for _ in range(3))
+            nat.check(nat.lib.az_engine_geometry(h, ctypes.byref(G), ctypes.byref(C),
+                                                 ctypes.byref(T)), "az_engine_geometry")
+            self.G, self.C, self.T = G.value, C.value, T.value
+            d = self.device
+            self.nn_in = torch.zeros(self.G, 64, dtype=torch.float32, device=d)
+            self.leaf = torch.full((self.G,), -1, dtype=torch.int32, device=d)
+            self.priors = torch.zeros(self.G, 65, dtype=torch.float32, device=d)
+            self.values = torch.zeros(self.G, dtype=torch.float32, device=d)
+
+    def close(self):
+        if getattr(self, "h", None):
+            nat.lib.az_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- async step pieces (current torch stream) -----------------------------------
+    def _s(self):
+        return nat.stream_ptr()
+
+    def select(self):
+        nat.check(nat.lib.az_select(self.h, nat.ptr(self.nn_in), nat.ptr(self.leaf), self._s()),
+                  "az_select")
+
+    def expand(self, priors=None, values=None):
+        pr = self.priors if priors is None else priors
+        va = self.values if values is None else values
+        assert pr.dtype == torch.float32 and pr.is_contiguous() and pr.shape == (self.G, 65)
+        assert va.dtype == torch.float32 and va.is_contiguous() and va.numel() == self.G
+        nat.check(nat.lib.az_expand_backup(self.h, nat.ptr(pr), nat.ptr(va), self._s()),
+                  "az_expand_backup")
+
+    def play(self):
+        nat.check(nat.lib.az_play(self.h, self._s()), "az_play")
+
+    # ---- synchronous control --------------------------------------------------------
+    def reset_all(self, start_budget=-1, stagger_steps=0):
+        nat.check(nat.lib.az_reset_all(self.h, int(start_budget), int(stagger_steps), self._s()),
+                  "az_reset_all")
+
+    def set_root(self, slot, own, opp, player):
+        nat.check(nat.lib.az_set_root(self.h, int(slot), int(own), int(opp), int(player),
+                                      self._s()), "az_set_root")
+
+    def begin_search(self, slot, sims):
+        nat.check(nat.lib.az_begin_search(self.h, int(slot), int(sims), self._s()),
+                  "az_begin_search")
+
+    def inject(self, noise=None, uniforms=None):
+        n = None if noise is None else np.ascontiguousarray(noise, np.float64)
+        u = None if uniforms is None else np.ascontiguousarray(uniforms, np.float64)
+        nat.check(nat.lib.az_inject(self.h, nat.ptr(n), nat.ptr(u), self._s()), "az_inject")
+
+    def root_policy(self, slot, temp, u_tie=0.0):
+        pi = np.zeros(65, np.float32)
+        counts = np.zeros(65, np.int32)
+        v = ctypes.c_double()
+        nat.check(nat.lib.az_root_policy(self.h, int(slot), float(temp), float(u_tie),
+                                         nat.ptr(pi), nat.ptr(counts), ctypes.byref(v),
+                                         self._s()), "az_root_policy")
+        return pi, counts, v.value
+
+    def make_move(self, slot, action):
+        nat.check(nat.lib.az_make_move(self.h, int(slot), int(action), self._s()),
+                  "az_make_move")
+
+    def counters(self):
+        out = np.zeros(8, np.int64)
+        nat.check(nat.lib.az_counters(self.h, nat.ptr(out), self._s()), "az_counters")
+        keys = ("games_started", "games_finished", "samples", "samples_dropped",
+                "arena_overflows", "steps", "simulations", "moves")
+        return dict(zip(keys, (int(x) for x in out)))
+
+    def game_info(self):
+        arrs = [np.zeros(self.G, np.int32) for _ in range(6)]
+        nat.check(nat.lib.az_game_info(self.h, *[nat.ptr(a) for a in arrs], self._s()),
+                  "az_game_info")
+        return dict(zip(("status", "ply", "winner", "root_player", "n_nodes", "overflow"),
+                        arrs))
+
+    def export_tree(self, slot, max_nodes=None):
+        n = ctypes.c_int32()
+        nat.check(nat.lib.az_export_tree(self.h, int(slot), 0, *([None] * 12),
+                                         ctypes.byref(n), self._s()), "az_export_tree")
+        m = n.value if max_nodes is None else min(n.value, max_nodes)
+        t = {"own": np.zeros(m, np.uint64), "opp": np.zeros(m, np.uint64),
+             "legal": np.zeros(m, np.uint64), "N": np.zeros(m, np.int32),
+             "W": np.zeros(m, np.float64), "prior": np.zeros(m, np.float64),
+             "parent": np.zeros(m, np.int32), "first": np.zeros(m, np.int32),
+             "nchild": np.zeros(m, np.uint8), "action": np.zeros(m, np.uint8),
+             "flags": np.zeros(m, np.uint8), "tval": np.zeros(m, np.int8)}
+        nat.check(nat.lib.az_export_tree(self.h, int(slot), m, *[nat.ptr(t[k]) for k in t],
+                                         ctypes.byref(n), self._s()), "az_export_tree")
+        t["n_nodes"] = n.value
+        return t
+
+    def export_trajectory(self, slot):
+        T = self.T
+        own, opp = np.zeros(T, np.uint64), np.zeros(T, np.uint64)
+        pi, player = np.zeros((T, 65), np.float32), np.zeros(T, np.int8)
+        vroot, n = np.zeros(T, np.float64), ctypes.c_int32()
+        nat.check(nat.lib.az_export_trajectory(self.h, int(slot), T, nat.ptr(own), nat.ptr(opp),
+                                               nat.ptr(pi), nat.ptr(player), nat.ptr(vroot),
+                                               ctypes.byref(n), self._s()),
+                  "az_export_trajectory")
+        k = n.value
+        return {"own": own[:k], "opp": opp[:k], "pi": pi[:k], "player": player[:k],
+                "vroot": vroot[:k]}
+
+    def samples(self, start=0, n=None, device=False):
+        """Sample rows [start, start+n) as numpy (device=False) or torch device tensors."""
+        if n is None:
+            n = self.counters()["samples"] - start
+        if device:
+            out = {"own": torch.empty(n, dtype=torch.int64, device=self.device),
+                   "opp": torch.empty(n, dtype=torch.int64, device=self.device),
+                   "pi": torch.empty(n, 65, dtype=torch.float32, device=self.device),
+                   "z": torch.empty(n, dtype=torch.float64, device=self.device),
+                   "player": torch.empty(n, dtype=torch.int8, device=self.device),
+                   "slot": torch.empty(n, dtype=torch.int32, device=self.device)}
+        else:
+            out = {"own": np.zeros(n, np.uint64), "opp": np.zeros(n, np.uint64),
+                   "pi": np.zeros((n, 65), np.float32), "z": np.zeros(n, np.float64),
+                   "player": np.zeros(n, np.int8), "slot": np.zeros(n, np.int32)}
+        nat.check(nat.lib.az_copy_samples(self.h, int(start), int(n),
+                                          *[nat.ptr(out[k]) for k in SAMPLE_FIELDS],
+                                          self._s()), "az_copy_samples")
+        return out
+
+    def clear_samples(self):
+        nat.check(nat.lib.az_clear_samples(self.h, self._s()), "az_clear_samples")
+
+
+def samples_to_tuples(s):
+    """Device sample rows -> the reference's training tuples
+    [(state int8 (8,8), pi float32 (65,), G float)] (self_play_worker.py:33-35), with
+    state = canonical board state*player (own stones +1)."""
+    n = len(s["z"])
+    ones = np.ones(n, np.int8)
+    boards = nat.unpack_np(s["own"], s["opp"], ones)
+    return [(boards[i], s["pi"][i].copy(), float(s["z"][i])) for i in range(n)]
+
+
+class BatchedSelfPlay:
+    """G concurrent self-play games on one GPU with a policy/value net.
+
+    `net` is any module with the reference forward signature ([B,1,8,8] -> (logits [B,65],
+    value [B,1])); it is evaluated through `Models.inference_copy` (BatchNorm folded,
+    channels-last, optional fp16 = config #5).  `args` uses the reference's keys
+    (train.py:399-423): c_puct, num_simulations, dirichlet_alpha, dirichlet_epsilon,
+    mcts_temperature, num_exploratory_moves, lambda.
+    """
+
+    def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
+                 dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
+                 device=None, fold=True):
+        from Models import inference_copy
+
+        self.args = dict(args)
+        self.engine = Engine(
+            n_games, args["num_simulations"], c_puct=args["c_puct"],
+            dirichlet_alpha=args.get("dirichlet_alpha", 1.0),
+            dirichlet_epsilon=args.get("dirichlet_epsilon", 0.0),
+            temperature=args.get("mcts_temperature", 1.0),
+            num_exploratory_moves=args.get("num_exploratory_moves", 0),
+            lambd=args.get("lambda", 1.0), rollout=net is None, d4_augment=d4_augment,
+            auto_play=True, refill=True, node_capacity=node_capacity,
+            sample_capacity=sample_capacity, seed=seed, stream_id=stream_id, device=device)
+        self.device = self.engine.device
+        if net is None:
+            self.net = None
+        elif fold:
+            self.net = inference_copy(net, self.device, dtype)
+        else:
+            self.net = net.to(self.device).eval()
+        self.use_graph = use_graph
+        self.graph = None
+
+    def _step_body(self):
+        e = self.engine
+        e.select()
+        if self.net is not None:
+            pr, va = self.net.evaluate_planes(e.nn_in)
+            e.priors.copy_(pr)
+            e.values.copy_(va)
+        e.expand()
+        e.play()
+
+    def _capture(self):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm MIOpen / hipBLASLt solution caches outside capture
+                self._step_body()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(g):
+            self._step_body()
+        self.graph = g
+
+    def reset(self, start_budget=-1, stagger_steps=0):
+        self.engine.reset_all(start_budget, stagger_steps)
+
+    @torch.no_grad()
+    def step(self, n=1):
+        if self.use_graph and self.graph is None:
+            try:
+                self._capture()
+            except Exception as ex:  # capture unsupported for this net: run eagerly
+                self.use_graph = False
+                self.graph_error = repr(ex)
+        for _ in range(n):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._step_body()
+
+    def play_games(self, n_games, max_steps=None, check_every=256):
+        """Play exactly n_games complete games (slots restart until the budget is used);
+        returns the reference's training tuples of every game."""
+        e = self.engine
+        self.reset(start_budget=n_games)
+        limit = max_steps or (n_games // max(1, e.G) + 2) * 200 * (self.args["num_simulations"] + 2)
+        done = 0
+        steps = 0
+        while done < n_games and steps < limit:
+            self.step(check_every)
+            steps += check_every
+            done = e.counters()["games_finished"]
+        return samples_to_tuples(e.samples())

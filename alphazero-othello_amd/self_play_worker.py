@@ -1,0 +1,80 @@
+"""Self-play driver drop-in (reference self_play_worker.py:1-88).
+
+`get_training_data` is the reference's TD(lambda) target rule (host copy of what the
+engine's finish kernel computes on device for batched self-play).  `one_self_play` keeps
+the reference's signature so train.py's process pool (train.py:199-225) works unchanged;
+the game itself runs through the MCTS drop-in on the GPU engine.  `collect_self_play_games`
+is the batched replacement for that whole pool: one engine, G concurrent games on the GPU.
+"""
+import numpy as np
+import torch
+
+from envs.othello import OthelloGameNew as OthelloGame
+from MCTS_model import MCTS
+
+
+def get_training_data(trajectory, winning_player, lambd: float = 1.0):
+    """G_T = z(player_T); G_t = (1-lambda) v_t + lambda * s * G_{t+1} with s = +1 when the
+    side to move is unchanged between t and t+1 (around a pass), else -1
+    (self_play_worker.py:8-35)."""
+
+    def z_for(p):
+        if winning_player == 0:
+            return 0.0
+        return 1.0 if p == winning_player else -1.0
+
+    out = [None] * len(trajectory)
+    g_next = None
+    p_next = None
+    for t in range(len(trajectory) - 1, -1, -1):
+        state, pi, player, v_root = trajectory[t]
+        if g_next is None:
+            g = z_for(player)
+        else:
+            s = 1.0 if player == p_next else -1.0
+            g = (1.0 - lambd) * v_root + lambd * s * g_next
+        out[t] = (state, pi, g)
+        g_next, p_next = g, player
+    return out
+
+
+@torch.no_grad()
+def one_self_play(args_tuple):
+    """One complete game (self_play_worker.py:38-88); returns [(state, pi, G)]."""
+    board_size, args, policy_state, inference_cache = args_tuple
+    env = OthelloGame(board_size)
+    policy_class, policy_config, policy_state_dict = policy_state
+    policy = policy_class(**policy_config)
+    policy.load_state_dict(policy_state_dict)
+    policy.eval()
+    mcts = MCTS(env, args, policy, dirichlet_alpha=args["dirichlet_alpha"],
+                dirichlet_epsilon=args["dirichlet_epsilon"], inference_cache=inference_cache)
+    trajectory = []
+    state = env.get_initial_state()
+    player = 1
+    while True:
+        temp = args["mcts_temperature"] if len(trajectory) < args["num_exploratory_moves"] else 0.0
+        probs = mcts.policy_improve_step(state, player, temp=temp)
+        trajectory.append((state.copy() * player, probs.copy(), player, mcts.root.value))
+        action = np.random.choice(env.action_size, p=probs)
+        mcts.make_move(action)
+        state = env.get_next_state(state, action, player)
+        reward, done = env.get_value_and_terminated(state, action, player)
+        if done:
+            winner = player if reward > 0 else (-player if reward < 0 else 0)
+            return get_training_data(trajectory, winner, args["lambda"])
+        player = env.get_opponent(player)
+
+
+def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, stream_id=0,
+                            d4_augment=False, dtype=torch.float32):
+    """Batched replacement of Trainer.collect_self_play_games' pool (train.py:199-225):
+    `num_games` games on one GPU, `n_slots` at a time (default min(num_games, 4096)).
+    Returns the concatenated training tuples of all games."""
+    from engine import BatchedSelfPlay
+
+    n_slots = n_slots or min(num_games, 4096)
+    sp = BatchedSelfPlay(policy, args, n_slots, seed=seed, stream_id=stream_id,
+                         d4_augment=d4_augment, dtype=dtype,
+                         sample_capacity=num_games * 130)
+    return sp.play_games(num_games)

@@ -1,0 +1,289 @@
+"""Self-play throughput benchmark: games/sec at 400 MCTS simulations per move.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU, RCCL)
+
+Workload (BASELINE.json configs[2], the one the metric is quoted on): 8x8 Othello,
+400 sims/move, AlphaZeroNet(8, 65, 5, 128) random init (no checkpoints offline), leaf batch
+1,024 = 1,024 concurrent games per GPU with one leaf each per step; the reference's
+self-play settings (train.py:399-423): c_puct 2, Dirichlet alpha 1 / eps 0.3 at the root,
+temperature 1 for 35 plies then 0, lambda 0.98.  fp32 throughout (the reference's dtype).
+
+A step is one batched simulation over every game slot: select (descent + leaf pack) ->
+net forward -> expand+backup -> move phase; games restart as they finish (weak scaling:
+1,024 games per GPU).  Slots start staggered over the warmup so moves complete at a
+steady rate.  value = (moves completed by all ranks in the timed window / mean plies per
+game) / window seconds (the window also contains the per-generation RCCL all-gather of
+the finished games' samples); games that actually finished in the window are reported
+beside it.
+
+Also measured in the same run:
+  roofline      the bitboard-step kernel (oth_step_gpu, the north-star kernel) on 2^24
+                positions drawn from this run's self-play states: 43 algorithmic bytes per
+                position (read own, opp, act = 17; write own', opp', legal, status = 26),
+                HIP events on the launch stream; traffic = HBM bytes from rocprofv3 PMC
+                (profiles/), or null.
+  cpu_baseline  the oracle's restatement of the reference self-play (oracle/selfplay.py:
+                sequential MCTS, batch-1 torch-CPU inference of the same net, the C board
+                oracle) on 1 host core for a bounded sample of moves.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "alphazero-othello_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+SELFPLAY_ARGS = {"c_puct": 2.0, "num_simulations": 400, "dirichlet_alpha": 1.0,
+                 "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0,
+                 "num_exploratory_moves": 35, "lambda": 0.98}
+REF_PLIES_PER_GAME = 60.0  # SURVEY.md 6 (measured on the reference at 400 sims)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STEP_BYTES = 43            # algorithmic bytes per board step
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--warmup", type=int, default=1200)
+    ap.add_argument("--games", type=int, default=1024, help="concurrent games per GPU")
+    ap.add_argument("--sims", type=int, default=400)
+    ap.add_argument("--net", default="az5x128", choices=["az5x128", "fast"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--kernel-n", type=int, default=1 << 24)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--skip-kernel", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "oth_step_traffic.json"))
+    return ap.parse_args()
+
+
+def make_net(kind):
+    from Models import AlphaZeroNet, FastOthelloNet
+
+    torch.manual_seed(0)
+    return AlphaZeroNet(8, 65, 5, 128) if kind == "az5x128" else FastOthelloNet(8, 65)
+
+
+def kernel_roofline(positions, n, device):
+    """Time oth_step_gpu over n positions resident in HBM."""
+    import az_native as nat
+
+    own, opp = positions
+    rng = np.random.default_rng(0)
+    # one legal action (or pass) per distinct position, then tile to n
+    lg = nat.legal_cpu(own, opp)
+    act = np.empty(len(own), np.uint8)
+    for i, m in enumerate(lg):
+        m = int(m)
+        if m == 0:
+            act[i] = 64
+        else:
+            bits = [b for b in range(64) if (m >> b) & 1]
+            act[i] = bits[int(rng.integers(0, len(bits)))]
+    reps = -(-n // len(own))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.tile(a, reps)[:n])).to(device)
+    d_own, d_opp = t(own.view(np.int64)), t(opp.view(np.int64))
+    d_act = t(act)
+    outs = [torch.empty(n, dtype=torch.int64, device=device) for _ in range(3)]
+    st = torch.empty(n, dtype=torch.int16, device=device)
+    s = nat.stream_ptr()
+    args = [nat.ptr(d_own), nat.ptr(d_opp), nat.ptr(d_act)] + [nat.ptr(x) for x in outs] + \
+        [nat.ptr(st), n, s]
+    for _ in range(3):
+        nat.check(nat.lib.oth_step_gpu(*args), "oth_step_gpu")
+    torch.cuda.synchronize()
+    reps_t = 20
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps_t):
+        nat.lib.oth_step_gpu(*args)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / reps_t
+    # spot-check the timed outputs against the host build of the same entry point
+    k = min(n, 1 << 16)
+    co, cp, cl, cs = nat.step_cpu(np.tile(own, reps)[:k], np.tile(opp, reps)[:k],
+                                  np.tile(act, reps)[:k], raise_illegal=False)
+    assert (outs[0][:k].cpu().numpy().view(np.uint64) == co).all()
+    return ms, n
+
+
+def cpu_baseline(net, seconds):
+    """The oracle's restatement of one_self_play (reference algorithm, sequential MCTS,
+    batch-1 torch-CPU inference, C board oracle), timed for a bounded sample of moves of one
+    game on one core; games/s = 1 / (seconds per move x plies per game)."""
+    from oracle import board as ob
+    from oracle.mcts import SeqMCTS
+
+    torch.set_num_threads(1)
+    cpu_net = net.cpu().eval()
+
+    def evaluate(own, opp, player):
+        s = ob.to_state(own, opp, player)
+        x = torch.from_numpy((player * s).astype(np.float32)).unsqueeze(0)
+        with torch.no_grad():
+            logits, v = cpu_net(x)
+            p = torch.softmax(logits, -1)
+        return p[0].numpy(), float(v[0, 0])
+
+    np.random.seed(0)
+    a = SELFPLAY_ARGS
+    m = SeqMCTS(a["c_puct"], a["num_simulations"], evaluate, dirichlet_alpha=a["dirichlet_alpha"],
+                dirichlet_epsilon=a["dirichlet_epsilon"])
+    game = ob.OracleGame()
+    state, player = game.get_initial_state(), 1
+    t0 = time.perf_counter()
+    moves = 0
+    while time.perf_counter() - t0 < seconds:
+        own, opp = ob.to_bitboards(state, player)
+        pi = m.search(own, opp, player, 1.0)
+        action = int(np.random.choice(65, p=pi))
+        m.make_move(action)
+        state = game.get_next_state(state, action, player)
+        moves += 1
+        if game.get_value_and_terminated(state, action, player)[1]:
+            break
+        player = -player
+    dt = time.perf_counter() - t0
+    per_move = dt / moves
+    return {"value": 1.0 / (per_move * REF_PLIES_PER_GAME), "unit": "games/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{moves} moves of one self-play game at 400 sims, AlphaZeroNet(5,128) "
+                      f"fp32 batch-1 torch-CPU, oracle/mcts.py SeqMCTS; {dt:.1f}s; "
+                      f"games/s = 1/(s_per_move x {REF_PLIES_PER_GAME:.0f} plies)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=device)
+
+    from engine import BatchedSelfPlay
+
+    net = make_net(a.net)
+    args = dict(SELFPLAY_ARGS, num_simulations=a.sims)
+    sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
+                         use_graph=not a.no_graph, device=device,
+                         sample_capacity=a.games * 130 * 4)
+    e = sp.engine
+    sp.reset(start_budget=-1, stagger_steps=max(a.warmup, 1))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    sp.step(a.warmup)
+    barrier()
+    c0 = e.counters()
+    t0 = time.perf_counter()
+    sp.step(a.steps)
+    # per-generation exchange: all-gather the finished games' samples over RCCL/xGMI
+    c_mid = e.counters()
+    n_new = c_mid["samples"] - c0["samples"]
+    allgather_rows = n_new
+    if dist is not None:
+        smp = e.samples(c0["samples"], n_new, device=True)
+        cnt = torch.tensor([n_new], device=device, dtype=torch.int64)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        mx = int(max(int(c) for c in cnts))
+        rec = torch.zeros(mx, 2 + 65 + 2, dtype=torch.float64, device=device)
+        if n_new:
+            rec[:n_new, 0] = smp["own"].view(torch.float64)
+            rec[:n_new, 1] = smp["opp"].view(torch.float64)
+            rec[:n_new, 2:67] = smp["pi"].double()
+            rec[:n_new, 67] = smp["z"]
+            rec[:n_new, 68] = smp["player"].double()
+        out = torch.empty(world * mx, rec.shape[1], dtype=rec.dtype, device=device)
+        dist.all_gather_into_tensor(out, rec)
+        allgather_rows = int(sum(int(c) for c in cnts))
+    barrier()
+    dt = time.perf_counter() - t0
+    c1 = e.counters()
+    moves = c1["moves"] - c0["moves"]
+    games_done = c1["games_finished"] - c0["games_finished"]
+    sims = c1["simulations"] - c0["simulations"]
+    plies_total = c1["samples"]
+    games_total = c1["games_finished"]
+    stats = torch.tensor([moves, games_done, sims, plies_total, games_total, dt],
+                         dtype=torch.float64, device=device)
+    if dist is not None:
+        allst = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(allst, stats)
+        allst = torch.stack(allst).cpu().numpy()
+    else:
+        allst = stats.cpu().numpy()[None]
+    moves_all, games_all, sims_all = allst[:, 0].sum(), allst[:, 1].sum(), allst[:, 2].sum()
+    plies_all, gtot_all = allst[:, 3].sum(), allst[:, 4].sum()
+    t_max = float(allst[:, 5].max())
+    plies_per_game = plies_all / gtot_all if gtot_all >= 16 else REF_PLIES_PER_GAME
+    value = moves_all / plies_per_game / t_max
+
+    result = {
+        "metric": "self-play games/sec (whole node), 8x8 Othello @ 400 MCTS sims/move",
+        "value": round(float(value), 4), "unit": "games/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(t_max * 1000.0 / a.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (net), int64 bitboards",
+        "data": "synthetic: self-play from the initial position, random-init net weights",
+        "config": {"workload": "configs[2]: 8x8 Othello, 400 sims/move, AlphaZeroNet(5x128) "
+                               "random init, leaf batch = concurrent games",
+                   "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
+                   "parallelism": f"dp{world} (independent games per GPU)",
+                   "hip_graph": sp.graph is not None},
+        "detail": {"moves": int(moves_all), "games_finished_in_window": int(games_all),
+                   "simulations": int(sims_all), "plies_per_game": round(float(plies_per_game), 2),
+                   "sims_per_s": round(float(sims_all / t_max), 1),
+                   "window_s": round(t_max, 3), "allgather_rows": allgather_rows,
+                   "arena_overflows": int(c1["arena_overflows"])},
+    }
+    if rank == 0 and world == 1 and not a.skip_kernel:
+        smp = e.samples(0, min(c1["samples"], 200000))
+        if len(smp["own"]) < 1024:
+            smp = {"own": np.array([0x0000000810000000], np.uint64),
+                   "opp": np.array([0x0000001008000000], np.uint64)}
+        ms, n = kernel_roofline((smp["own"], smp["opp"]), a.kernel_n, device)
+        achieved = STEP_BYTES * n / (ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                traffic = json.load(open(a.traffic_json)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result["roofline"] = {"kernel": "oth_step_gpu (k_step)", "bound": "hbm",
+                              "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                              "traffic": traffic, "positions": n,
+                              "avg_launch_ms": round(ms, 4),
+                              "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
+    if rank == 0 and world == 1 and not a.skip_cpu:
+        result["cpu_baseline"] = cpu_baseline(make_net(a.net), a.cpu_seconds)
+        result["cpu_baseline"]["cores"] = 1
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -66,6 +66,12 @@ int oth_step_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
                  uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
                  int64_t n);
 
+/* raw make-move without a legality check (pass = swap sides): replaces
+ * _BitBoard.make_move (envs/othello.py:171-200), which places an unbounded stone with no
+ * captures.  Outputs are the next side's (own, opp). */
+int oth_make_move_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                      uint64_t* own_o, uint64_t* opp_o, int64_t n);
+
 /* int8 (n,8,8) absolute-colour states + int8 player[n] -> (own, opp) bitboards where
  * own = stones equal to player.  Replaces OthelloGameNew._np_to_bitboards
  * (envs/othello.py:358-371) in the row-major layout (no 180-degree rotation). */
@@ -92,111 +98,136 @@ int oth_d4_gpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n,
                void* stream);
 
 /* ---------------- batched MCTS self-play engine (device) -------------------------
- * G game slots, each with its own flat SoA node arena (tree of reference `Node`s,
- * MCTS_model.py:46-169) and trajectory buffer.  One sim-step = az_select (descend every
- * game's tree to one leaf, PUCT of MCTS_model.py:129-139 / :362-370; terminal leaves are
- * backed up in place) -> caller evaluates the leaves (policy/value net) -> az_expand_backup
- * (MCTS_model.py:325-360 eager expansion + backup :160-169).  With one leaf per game per
- * step the search is exactly the reference with args['num_threads'] = 1. */
+ * G game slots, each with its own flat SoA node arena (the reference's `Node` tree,
+ * MCTS_model.py:46-169) in two ping-pong halves (live tree + re-root compaction target),
+ * and a trajectory buffer.  One simulation step, all asynchronous on `stream` and
+ * graph-capturable (no host synchronisation, no allocation):
+ *   az_select        descend every active slot's tree to one leaf (PUCT of
+ *                    MCTS_model.py:129-139 / :362-370; terminal leaves are backed up in
+ *                    place, :381-384) and pack the leaf's canonical NN input;
+ *   (caller)         policy/value net on nn_in -> priors (softmax), values (tanh);
+ *   az_expand_backup eager expansion + backup (MCTS_model.py:325-360, :160-169);
+ *   az_play          auto-play engines: every slot whose search finished plays its move
+ *                    (pi, record, sample, move, terminal check, TD(lambda) targets, re-root;
+ *                    MCTS_model.py:200-274, self_play_worker.py:8-88) and finished slots
+ *                    restart while the start budget lasts.  Host-driven engines: only
+ *                    advances the step counter.
+ * With one leaf per slot per step the search is exactly the reference with
+ * args['num_threads'] = 1. */
 
 typedef struct az_engine az_engine;
 
 enum { AZ_EVAL_EXTERNAL = 0, AZ_EVAL_ROLLOUT = 1 };
 enum { AZ_RNG_DEVICE = 0, AZ_RNG_INJECTED = 1 };
-enum { AZ_GAME_IDLE = 0, AZ_GAME_ACTIVE = 1, AZ_GAME_FINISHED = 2 };
+enum { AZ_GAME_IDLE = 0, AZ_GAME_ACTIVE = 1, AZ_GAME_FINISHED = 2, AZ_GAME_SEARCH_DONE = 3 };
 
 typedef struct az_config {
   int32_t n_games;               /* G concurrent game slots */
-  int32_t node_capacity;         /* arena nodes per game (0 -> 16384) */
+  int32_t node_capacity;         /* arena nodes per slot and half (0 -> 16384; <= 32768) */
   int32_t max_plies;             /* trajectory capacity per game (0 -> 128) */
   int32_t num_simulations;       /* args['num_simulations'] */
   double c_puct;                 /* args['c_puct'] */
   double dirichlet_alpha;        /* self_play_worker.py:56 */
   double dirichlet_epsilon;      /* self_play_worker.py:57; 0 disables root noise */
-  double temperature;            /* args['mcts_temperature'] (self_play_worker.py:61) */
+  double temperature;            /* args['mcts_temperature'] (self_play_worker.py:66-67) */
   int32_t num_exploratory_moves; /* args['num_exploratory_moves'] */
   double lambd;                  /* args['lambda'] (TD(lambda), self_play_worker.py:8-35) */
   int32_t eval_mode;             /* AZ_EVAL_EXTERNAL (net) or AZ_EVAL_ROLLOUT (policy None) */
   int32_t rng_mode;              /* AZ_RNG_DEVICE (Philox) or AZ_RNG_INJECTED (parity) */
   int32_t d4_augment;            /* 1: random D4 transform per leaf in the NN input pack,
                                     inverse-mapped priors (config #5) */
-  int32_t refill;                /* 1: finished games restart from the initial position */
+  int32_t auto_play;             /* 1: az_play plays moves on device (batched self-play);
+                                    0: the host drives moves (MCTS class API) */
+  int32_t refill;                /* auto-play: finished slots restart a fresh game */
+  int64_t sample_capacity;       /* rows of the device sample buffer (0 -> 2*G*max_plies) */
+  int32_t inj_noise_slots;       /* AZ_RNG_INJECTED: Dirichlet vectors per slot */
+  int32_t inj_uniform_slots;     /* AZ_RNG_INJECTED: uniforms per slot */
   uint64_t seed;                 /* Philox key */
   uint64_t stream_id;            /* Philox sub-stream (rank) */
 } az_config;
 
 int az_engine_create(const az_config* cfg, az_engine** out);
 int az_engine_destroy(az_engine* eng);
+int az_engine_geometry(az_engine* eng, int32_t* n_games, int32_t* node_capacity,
+                       int32_t* max_plies);
 
 /* every slot -> a fresh game at the initial position, player +1 (self_play_worker.py:
- * 55-57).  Synchronous. */
-int az_reset_all(az_engine* eng, void* stream);
-/* slot -> root at an arbitrary position (MCTS.policy_improve_step with root None,
- * MCTS_model.py:223-228).  Synchronous.  player in {+1,-1}. */
+ * 59-61).  start_budget < 0: unlimited restarts; else at most start_budget games are ever
+ * started (slots beyond it stay idle).  Slot g becomes active at step g*stagger/G.
+ * Resets the counters.  Synchronous. */
+int az_reset_all(az_engine* eng, int64_t start_budget, int32_t stagger_steps, void* stream);
+
+/* slot -> root at an arbitrary position, tree discarded (MCTS.policy_improve_step with
+ * root None, MCTS_model.py:223-228).  player in {+1,-1}.  Synchronous. */
 int az_set_root(az_engine* eng, int32_t slot, uint64_t own, uint64_t opp, int32_t player,
                 void* stream);
-/* start a search: sims counter := 0 for every active slot (MCTS_model.py:237). */
-int az_begin_search(az_engine* eng, int32_t num_simulations, void* stream);
 
-/* one leaf per active slot whose search is not done.  nn_in: float [G,64], the
- * canonical input player*state (Models.py:16) of the leaf, zeros for slots without a
- * leaf.  leaf_o (optional, int32 [G]): leaf node index or -1. */
+/* start a search of num_simulations on one slot (or all, slot = -1): MCTS_model.py:237. */
+int az_begin_search(az_engine* eng, int32_t slot, int32_t num_simulations, void* stream);
+
+/* one leaf per active slot.  nn_in: float [G,64], canonical player*state (Models.py:16)
+ * of the leaf, zeros for slots without a leaf.  leaf_o (optional, int32 [G]): leaf node
+ * index or -1. */
 int az_select(az_engine* eng, float* nn_in, int32_t* leaf_o, void* stream);
 
-/* priors: float [G,65] (softmax output), values: float [G] (tanh output), ignored in
- * rollout mode.  noise: double [G,65] Dirichlet vectors for AZ_RNG_INJECTED (may be NULL
- * when epsilon is 0).  Expands every pending leaf and backs up its value. */
-int az_expand_backup(az_engine* eng, const float* priors, const float* values,
-                     const double* noise, void* stream);
+/* priors: float [G,65] (softmax output), values: float [G] (tanh output); both ignored
+ * in rollout mode. */
+int az_expand_backup(az_engine* eng, const float* priors, const float* values, void* stream);
 
-/* pi from root visit counts (MCTS_model.py:244-274), trajectory record
- * (self_play_worker.py:67-73), action sample (self_play_worker.py:75).
- * u_tie/u_act: double [G] uniforms for AZ_RNG_INJECTED (NULL otherwise).
- * pi_o float [G,65], action_o int32 [G], vroot_o double [G]: optional outputs. */
-int az_root_policy(az_engine* eng, const double* u_tie, const double* u_act, float* pi_o,
-                   int32_t* action_o, double* vroot_o, void* stream);
+/* auto-play move phase (see above); host-driven engines: step counter only. */
+int az_play(az_engine* eng, void* stream);
 
-/* play the chosen (or given, action != NULL: int32 [G], -1 = chosen) action in every
- * active slot: re-root with subtree reuse (MCTS.make_move, MCTS_model.py:200-215),
- * terminal check from the mover's view (self_play_worker.py:77-86).  Compacts arenas. */
-int az_advance(az_engine* eng, const int32_t* action, void* stream);
+/* AZ_RNG_INJECTED: per-slot streams, noise double [G, inj_noise_slots, 65] (Dirichlet
+ * vectors, consumed at each root expansion with epsilon > 0) and uniforms double
+ * [G, inj_uniform_slots] (consumed by the temperature-0 tie break and the action sample,
+ * in the reference's np.random call order).  Resets the cursors.  Synchronous. */
+int az_inject(az_engine* eng, const double* noise, const double* uniforms, void* stream);
 
-/* finished games -> TD(lambda) targets (get_training_data, self_play_worker.py:8-35)
- * appended to the device sample buffer; with refill, their slots restart.
- * Returns (host) the number of games harvested in *n_games_o and total samples in the
- * device buffer in *n_samples_o.  Synchronous. */
-int az_harvest(az_engine* eng, int32_t* n_games_o, int64_t* n_samples_o, void* stream);
+/* pi of one slot's root (MCTS_model.py:244-271) at temperature `temp`; u_tie in [0,1)
+ * picks among tied maxima at temp < 0.1 (index floor(u_tie * n_ties)).  Optional outputs:
+ * counts int32[65] (child visit counts), vroot (root W/N).  Synchronous. */
+int az_root_policy(az_engine* eng, int32_t slot, double temp, double u_tie, float* pi_o,
+                   int32_t* counts_o, double* vroot_o, void* stream);
 
-/* device sample buffer (filled by az_harvest): own/opp u64 canonical board (state*player
- * of the recorded ply), pi float[65], z double, player int8.  Pointers are device
- * pointers owned by the engine; n <= capacity. */
-int az_samples(az_engine* eng, uint64_t** own, uint64_t** opp, float** pi, double** z,
-               int8_t** player, int64_t* n, int64_t* capacity);
-int az_clear_samples(az_engine* eng);
+/* re-root one slot on the child reached by `action`, keeping its subtree and statistics
+ * (MCTS.make_move, MCTS_model.py:200-215): AZ_ERR_STATE if the root has no such child
+ * (KeyError in the reference).  Synchronous. */
+int az_make_move(az_engine* eng, int32_t slot, int32_t action, void* stream);
 
-/* host copies of per-slot state: status (AZ_GAME_*), ply, winner (+1/-1/0), root player,
- * nodes in use, arena overflow count.  Any pointer may be NULL.  Synchronous. */
+/* counters: [games_started, games_finished, samples, samples_dropped, arena_overflows,
+ * steps, simulations, moves].  Synchronous. */
+int az_counters(az_engine* eng, int64_t* out8, void* stream);
+
+/* host copies of per-slot state (int32 [G] each): status (AZ_GAME_*), ply, winner
+ * (+1/-1/0), root player, nodes in use, arena overflow count.  Any pointer may be NULL. */
 int az_game_info(az_engine* eng, int32_t* status, int32_t* ply, int32_t* winner,
                  int32_t* root_player, int32_t* n_nodes, int32_t* overflow, void* stream);
 
-/* host copy of one slot's tree (n_nodes entries; root = node 0): bitboards, visit count,
- * value sum, prior, parent, first child, child count, action, flags (bit0 expanded,
- * bit1 terminal, bit2 f64 child priors), terminal value.  Any pointer may be NULL. */
+/* host copy of one slot's tree (root = node 0; children contiguous, ascending action):
+ * bitboards (side to move), visit count, value sum, prior, parent, first child, child
+ * count, action, flags (bit0 expanded, bit1 terminal, bit2 float64 child priors),
+ * terminal value.  Any pointer may be NULL.  Synchronous. */
 int az_export_tree(az_engine* eng, int32_t slot, int32_t max_nodes, uint64_t* own,
                    uint64_t* opp, uint64_t* legal, int32_t* N, double* W, double* prior,
                    int32_t* parent, int32_t* first_child, uint8_t* nchild, uint8_t* action,
                    uint8_t* flags, int8_t* tval, int32_t* n_nodes_o, void* stream);
 
-/* host copy of one slot's trajectory (ply entries): canonical own/opp, pi, player,
- * root value.  Synchronous. */
+/* host copy of one slot's trajectory: canonical own/opp (state*player,
+ * self_play_worker.py:72), pi float[65], player, root value.  Synchronous. */
 int az_export_trajectory(az_engine* eng, int32_t slot, int32_t max_plies, uint64_t* own,
                          uint64_t* opp, float* pi, int8_t* player, double* vroot,
                          int32_t* n_plies_o, void* stream);
 
-/* re-root one slot on the child reached by `action` (MCTS.make_move,
- * MCTS_model.py:200-215): AZ_ERR_STATE if the root has no such child (KeyError).
- * Synchronous. */
-int az_make_move(az_engine* eng, int32_t slot, int32_t action, void* stream);
+/* device sample buffer (TD(lambda) rows of finished games, get_training_data,
+ * self_play_worker.py:8-35): canonical own/opp u64, pi float[65], z double, player int8.
+ * Device pointers owned by the engine. */
+int az_samples(az_engine* eng, uint64_t** own, uint64_t** opp, float** pi, double** z,
+               int8_t** player, int64_t* n, int64_t* capacity);
+/* copy sample rows [start, start+n) to host or device buffers (any pointer may be NULL);
+ * slot = the game slot that produced each row.  Synchronous. */
+int az_copy_samples(az_engine* eng, int64_t start, int64_t n, uint64_t* own, uint64_t* opp,
+                    float* pi, double* z, int8_t* player, int32_t* slot, void* stream);
+int az_clear_samples(az_engine* eng, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,3 +59,17 @@ def mock_eval_planes(nn_in):
     x = np.rint(np.asarray(nn_in, np.float32)).astype(np.int64).reshape(-1, 64)
     p, v = mock_eval(x)
     return p, v.astype(np.float32)
+
+
+def mock_eval_torch(planes):
+    """The same closed form on device (torch float64 matmuls are exact here: every partial
+    sum is an integer below 2^53).  planes: float32 [G, 64] -> (priors f32 [G, 65],
+    values f32 [G])."""
+    import torch
+
+    x = torch.round(planes.double()) + 1.0
+    At = torch.as_tensor(A.T, dtype=torch.float64, device=planes.device)
+    Bt = torch.as_tensor(B, dtype=torch.float64, device=planes.device)
+    h = torch.remainder(x @ At, 1021.0) + 1.0
+    k = torch.remainder(x @ Bt, 2001.0)
+    return (h / 1024.0).float().contiguous(), ((k - 1000.0) / 1024.0).float().contiguous()
