@@ -148,9 +148,11 @@ def get_config(net):
     return net.get_config()
 
 
-def inference_copy(net: nn.Module, device, dtype=torch.float32) -> nn.Module:
+def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True) -> nn.Module:
     """An eval-mode copy of `net` on `device` for the batched engine: BatchNorm folded
     into the preceding convolution (same function in eval mode, fewer kernels per step).
+    With `fused` (fp32, AlphaZeroNet / FastOthelloNet) the convolutions run without bias
+    and one HIP epilogue kernel applies bias + residual + ReLU (csrc/nn_fused.hip).
     `dtype` float16 is config #5's fp16 inference."""
     import copy
 
@@ -158,7 +160,7 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32) -> nn.Module:
 
     def fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
         w = conv.weight.detach()
-        b = conv.bias.detach() if conv.bias is not None else torch.zeros(w.shape[0])
+        b = conv.bias.detach() if conv.bias is not None else torch.zeros(w.shape[0], device=w.device)
         scale = bn.weight.detach() / torch.sqrt(bn.running_var + bn.eps)
         conv.weight = nn.Parameter(w * scale[:, None, None, None])
         conv.bias = nn.Parameter((b - bn.running_mean) * scale + bn.bias.detach())
@@ -177,4 +179,80 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32) -> nn.Module:
                 seq[1] = fold(seq[0], seq[1])
     m = m.to(device=device, dtype=dtype)
     m = m.to(memory_format=torch.channels_last)
+    if fused and dtype == torch.float32 and isinstance(m, (AlphaZeroNet, FastOthelloNet)):
+        return FusedInferenceNet(m).eval()
     return m.eval()
+
+
+class _ConvEpilogue(nn.Module):
+    """conv2d without bias (MIOpen) + the fused bias/residual/ReLU epilogue kernel."""
+
+    def __init__(self, conv: nn.Conv2d):
+        super().__init__()
+        self.weight = nn.Parameter(conv.weight.detach().contiguous(
+            memory_format=torch.channels_last), requires_grad=False)
+        self.bias = nn.Parameter(conv.bias.detach().contiguous(), requires_grad=False)
+        self.padding = conv.padding
+
+    def forward(self, x, res=None, relu=True):
+        import az_native as nat
+
+        y = F.conv2d(x, self.weight, None, padding=self.padding)
+        if not y.is_contiguous(memory_format=torch.channels_last):
+            y = y.contiguous(memory_format=torch.channels_last)
+        if res is not None and not res.is_contiguous(memory_format=torch.channels_last):
+            res = res.contiguous(memory_format=torch.channels_last)
+        nat.check(nat.lib.az_bias_act_gpu(nat.ptr(y), nat.ptr(self.bias),
+                                          None if res is None else nat.ptr(res), y.numel(),
+                                          y.shape[1], int(relu), nat.stream_ptr()),
+                  "az_bias_act_gpu")
+        return y
+
+
+def _merge_1x1(a: nn.Conv2d, b: nn.Conv2d) -> nn.Conv2d:
+    m = nn.Conv2d(a.in_channels, a.out_channels + b.out_channels, 1)
+    m.weight = nn.Parameter(torch.cat([a.weight.detach(), b.weight.detach()], 0))
+    m.bias = nn.Parameter(torch.cat([a.bias.detach(), b.bias.detach()], 0))
+    return m.to(a.weight.device)
+
+
+class FusedInferenceNet(nn.Module, Inference):
+    """Inference-only form of AlphaZeroNet / FastOthelloNet with BatchNorm folded and every
+    conv epilogue fused (same function as the source net in eval mode)."""
+
+    def __init__(self, m: nn.Module):
+        super().__init__()
+        self.kind = "az" if isinstance(m, AlphaZeroNet) else "fast"
+        self.board_size = m.board_size
+        self.softmax = nn.Softmax(dim=-1)
+        if self.kind == "az":
+            self.stem = _ConvEpilogue(m.conv0)
+            blocks = list(m.res)
+            self.heads = _ConvEpilogue(_merge_1x1(m.pol_conv, m.val_conv))
+            self.n_pol = m.pol_conv.out_channels
+            self.pol_fc, self.val_fc1, self.val_fc2 = m.pol_fc, m.val_fc1, m.val_fc2
+        else:
+            self.stem = _ConvEpilogue(m.initial_conv[0])
+            blocks = [m.res_block]
+            self.tail = _ConvEpilogue(m.conv_add[0])
+            self.fc_policy, self.fc_value1, self.fc_value2 = m.fc_policy, m.fc_value1, m.fc_value2
+        self.c1 = nn.ModuleList([_ConvEpilogue(b.conv1) for b in blocks])
+        self.c2 = nn.ModuleList([_ConvEpilogue(b.conv2) for b in blocks])
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        x = x.contiguous(memory_format=torch.channels_last)
+        h = self.stem(x)
+        for c1, c2 in zip(self.c1, self.c2):
+            h = c2(c1(h), res=h)
+        B = h.shape[0]
+        if self.kind == "az":
+            y = self.heads(h)
+            p = y[:, :self.n_pol].reshape(B, -1)
+            v = y[:, self.n_pol:].reshape(B, -1)
+            v = torch.tanh(self.val_fc2(F.relu(self.val_fc1(v))))
+            return self.pol_fc(p), v
+        h = self.tail(h).reshape(B, -1)
+        v = torch.tanh(self.fc_value2(F.relu(self.fc_value1(h))))
+        return self.fc_policy(h), v

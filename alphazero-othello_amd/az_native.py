@@ -97,6 +97,7 @@ SIGNATURES = {
     "az_samples": [_P, _P, _P, _P, _P, _P, _P, _P],
     "az_copy_samples": [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
     "az_clear_samples": [_P, _P],
+    "az_bias_act_gpu": [_P, _P, _P, _I64, _I32, _I32, _P],
 }
 
 

@@ -229,6 +229,15 @@ int az_copy_samples(az_engine* eng, int64_t start, int64_t n, uint64_t* own, uin
                     float* pi, double* z, int8_t* player, int32_t* slot, void* stream);
 int az_clear_samples(az_engine* eng, void* stream);
 
+/* ---------------- leaf-evaluation net support (device) ---------------------------
+ * Fused conv epilogue of the inference copy of the policy/value net (reference
+ * Models.py:72-221 with BatchNorm folded): y = act(y + bias[c] (+ res)) in place over an
+ * NHWC (channels-last) float32 activation of n elements and `channels` channels; res may
+ * be NULL; relu 0/1.  Replaces the conv bias add, `out += residual` (Models.py:84-86) and
+ * F.relu as separate passes. */
+int az_bias_act_gpu(float* y, const float* bias, const float* res, int64_t n,
+                    int32_t channels, int32_t relu, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,7 +39,8 @@ def step_gpu(own, opp, act):
 def legal_gpu(own, opp):
     n = len(own)
     out = torch.empty(n, dtype=torch.int64, device="cuda")
-    nat.check(nat.lib.oth_legal_gpu(nat.ptr(dev(own)), nat.ptr(dev(opp)), nat.ptr(out), n,
+    d_own, d_opp = dev(np.asarray(own, np.uint64)), dev(np.asarray(opp, np.uint64))  # keep alive
+    nat.check(nat.lib.oth_legal_gpu(nat.ptr(d_own), nat.ptr(d_opp), nat.ptr(out), n,
                                     nat.stream_ptr()), "oth_legal_gpu")
     torch.cuda.synchronize()
     return host_u64(out)
@@ -136,7 +137,8 @@ def test_d4_device_matches_numpy_tables():
     x = rng.integers(0, 2**63, 4096, dtype=np.int64).astype(np.uint64)
     sym = rng.integers(0, 8, 4096).astype(np.uint8)
     out = torch.empty(4096, dtype=torch.int64, device="cuda")
-    nat.check(nat.lib.oth_d4_gpu(nat.ptr(dev(x)), nat.ptr(dev(sym)), nat.ptr(out), 4096,
+    d_x, d_sym = dev(x), dev(sym)  # keep the inputs alive across the async launch
+    nat.check(nat.lib.oth_d4_gpu(nat.ptr(d_x), nat.ptr(d_sym), nat.ptr(out), 4096,
                                  nat.stream_ptr()), "oth_d4_gpu")
     torch.cuda.synchronize()
     got = host_u64(out)

@@ -114,7 +114,7 @@ def test_selfplay_games_match_reference_on_device():
                    auto_play=True, refill=False, inj_noise_slots=1, inj_uniform_slots=NU)
         e.reset_all(start_budget=G)
         e.inject(noise=noise, uniforms=uni)
-        for _ in range(200):
+        for _ in range(1000):
             for _ in range(100):
                 e.select()
                 pr, va = mock_eval_torch(e.nn_in)
