@@ -1,0 +1,44 @@
+"""Build scripts/exp/step_variants.hip and time every variant on 2^24 positions."""
+import ctypes, json, os, subprocess, sys
+import numpy as np, torch
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+so = os.path.join(ROOT, "gpurun_out", "step_variants.so")
+os.makedirs(os.path.dirname(so), exist_ok=True)
+subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared",
+                       "-std=c++17", os.path.join(HERE, "step_variants.hip"), "-o", so])
+L = ctypes.CDLL(so)
+L.run_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 7 + [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+n = 1 << 24
+d = np.load(os.path.join(ROOT, "tests", "golden", "board_corpus.npz"))
+pl = d["player"]
+own = np.where(pl == 1, d["pos"], d["neg"]).astype(np.uint64)
+opp = np.where(pl == 1, d["neg"], d["pos"]).astype(np.uint64)
+act = d["action"].astype(np.uint8)
+k = -(-n // len(own))
+t = lambda a: torch.from_numpy(np.ascontiguousarray(np.tile(a, k)[:n])).cuda()
+I = [t(own.view(np.int64)), t(opp.view(np.int64)), t(act)]
+res = {}
+ref = None
+VARS = [int(x) for x in os.environ.get('VARIANTS', '0,1,2,3,4,5,6,7,8,9').split(',')]
+for v in VARS:
+    for grid in ((65536,) if v == 9 else (2048, 8192, 32768)):
+        O = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(3)] + [torch.zeros(n, dtype=torch.int16, device="cuda")]
+        args = [v] + [x.data_ptr() for x in I + O] + [n, grid, torch.cuda.current_stream().cuda_stream]
+        assert L.run_variant(*args) == 0
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        e0.record()
+        for _ in range(20):
+            L.run_variant(*args)
+        e1.record(); torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 20
+        ok = None
+        if v in (0, 2, 3, 7, 9):
+            outs = [o.cpu() for o in O]
+            if ref is None: ref = outs
+            ok = all(bool((a == b).all()) for a, b in zip(outs, ref))
+        if v in (5, 6):
+            ok = bool((O[2].cpu() == ref[2]).all()) if False else None
+        res[f"v{v}_g{grid}"] = {"ms": round(ms, 4), "gsteps": round(n / ms / 1e6, 1), "alg_TBps": round(43 * n / ms / 1e9, 3), "ok": ok}
+print(json.dumps(res, indent=0))

@@ -1,0 +1,159 @@
+// Experiment harness (not product code): variants of the batched board-step kernel, to find
+// what bounds k_step on gfx950.  Built on the GPU box by scripts/exp/run_step_variants.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../alphazero-othello_amd/csrc/bitboard.h"
+
+namespace x {
+using namespace azb;
+
+__device__ __forceinline__ uint64_t mk(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+template <int K> __device__ __forceinline__ uint64_t shl(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  return mk(lo << K, __builtin_amdgcn_alignbit(hi, lo, 32 - K));
+}
+template <int K> __device__ __forceinline__ uint64_t shr(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  return mk(__builtin_amdgcn_alignbit(hi, lo, K), hi >> K);
+}
+template <int D> __device__ __forceinline__ uint64_t moves_dir32(uint64_t P, uint64_t M) {
+  uint64_t fl = M & shl<D>(P);
+  uint64_t fr = M & shr<D>(P);
+  fl |= M & shl<D>(fl);
+  fr |= M & shr<D>(fr);
+  const uint64_t ml = M & shl<D>(M);
+  const uint64_t mr = shr<D>(ml);
+  fl |= ml & shl<2 * D>(fl);
+  fr |= mr & shr<2 * D>(fr);
+  fl |= ml & shl<2 * D>(fl);
+  fr |= mr & shr<2 * D>(fr);
+  return shl<D>(fl) | shr<D>(fr);
+}
+__device__ __forceinline__ uint64_t legal32(uint64_t own, uint64_t opp) {
+  const uint64_t inner = opp & kInner;
+  uint64_t m = moves_dir32<1>(own, inner);
+  m |= moves_dir32<8>(own, opp);
+  m |= moves_dir32<7>(own, inner);
+  m |= moves_dir32<9>(own, inner);
+  return m & ~(own | opp);
+}
+__device__ __forceinline__ Step step32(uint64_t own, uint64_t opp, int act) {
+  Step o;
+  int flags = 0;
+  if (act == kPass) { o.own = opp; o.opp = own; flags = kFlagPassed; }
+  else {
+    const bool in_range = (unsigned)act < 64u;
+    const int sq = act & 63;
+    const uint64_t nb = 1ull << sq;
+    const uint64_t cap = in_range ? flips(own, opp, sq) : 0ull;
+    if (!in_range || cap == 0ull || (nb & (own | opp))) {
+      o.own = own; o.opp = opp; o.legal = 0; o.status = pack_status(kFlagIllegal, 0); return o;
+    }
+    o.own = opp ^ cap; o.opp = (own | nb) ^ cap;
+  }
+  o.legal = legal32(o.own, o.opp);
+  if (!o.legal) flags |= legal32(o.opp, o.own) ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
+  o.status = pack_status(flags, popc(o.own) - popc(o.opp));
+  return o;
+}
+}  // namespace x
+
+#define GS for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+
+__global__ __launch_bounds__(256) void v0(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { azb::Step s = azb::step(own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+}
+__global__ __launch_bounds__(256) void v1(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { uint64_t a = own[i], b = opp[i]; int c = act[i]; oo[i] = a ^ c; po[i] = b; lo[i] = a | b; so[i] = (uint16_t)c; }
+}
+__global__ __launch_bounds__(256) void v2(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { azb::Step s = x::step32(own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+}
+// two positions per lane, 16-byte I/O
+__global__ __launch_bounds__(256) void v3(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t n2 = n / 2;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n2; j += (int64_t)gridDim.x * 256) {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2*>(own)[j];
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(opp)[j];
+    const uint16_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    azb::Step s0 = x::step32(a.x, b.x, c & 0xFF), s1 = x::step32(a.y, b.y, c >> 8);
+    reinterpret_cast<ulonglong2*>(oo)[j] = make_ulonglong2(s0.own, s1.own);
+    reinterpret_cast<ulonglong2*>(po)[j] = make_ulonglong2(s0.opp, s1.opp);
+    reinterpret_cast<ulonglong2*>(lo)[j] = make_ulonglong2(s0.legal, s1.legal);
+    reinterpret_cast<uint32_t*>(so)[j] = (uint32_t)s0.status | ((uint32_t)s1.status << 16);
+  }
+}
+// I/O only, 2 per lane
+__global__ __launch_bounds__(256) void v4(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t n2 = n / 2;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n2; j += (int64_t)gridDim.x * 256) {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2*>(own)[j];
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(opp)[j];
+    const uint16_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    reinterpret_cast<ulonglong2*>(oo)[j] = make_ulonglong2(a.x ^ c, a.y);
+    reinterpret_cast<ulonglong2*>(po)[j] = b;
+    reinterpret_cast<ulonglong2*>(lo)[j] = make_ulonglong2(a.x | b.x, a.y | b.y);
+    reinterpret_cast<uint32_t*>(so)[j] = c;
+  }
+}
+// legal only (no flips): compute cost of the legal mask alone, 64-bit shifts vs 32-bit
+__global__ __launch_bounds__(256) void v5(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { lo[i] = azb::legal(own[i], opp[i]); }
+}
+__global__ __launch_bounds__(256) void v6(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { lo[i] = x::legal32(own[i], opp[i]); }
+}
+
+// software-pipelined grid-stride: next iteration's inputs are loaded before this one's compute
+__global__ __launch_bounds__(256) void v7(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t a = own[i], b = opp[i]; int c = act[i];
+  for (; i < n; i += stride) {
+    const int64_t j = i + stride;
+    uint64_t a2 = 0, b2 = 0; int c2 = 0;
+    if (j < n) { a2 = own[j]; b2 = opp[j]; c2 = act[j]; }
+    azb::Step s = azb::step(a, b, c);
+    oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    a = a2; b = b2; c = c2;
+  }
+}
+// compute only: inputs synthesised from the index (a corpus-like mix is not needed for an
+// op count), one store per lane at the end
+__global__ __launch_bounds__(256) void v8(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t base_o = own[t & 32767], base_p = opp[t & 32767];
+  const int base_a = act[t & 32767];
+  uint64_t acc = 0;
+  for (int64_t i = t; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t r = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    azb::Step s = azb::step(base_o ^ (r & 0), base_p ^ (r & 0), (base_a + (int)(i >> 20)) & 63);
+    acc ^= s.own ^ s.opp ^ s.legal ^ s.status;
+  }
+  lo[t] = acc;
+}
+// one position per lane, no grid-stride loop
+__global__ __launch_bounds__(256) void v9(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) { azb::Step s = azb::step(own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+}
+
+extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
+  void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9};
+  if (v < 0 || v > 9) return -1;
+  hipLaunchKernelGGL(ks[v], dim3(grid), dim3(256), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
