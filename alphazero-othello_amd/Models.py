@@ -148,7 +148,8 @@ def get_config(net):
     return net.get_config()
 
 
-def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True) -> nn.Module:
+def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
+                   conv="hip") -> nn.Module:
     """An eval-mode copy of `net` on `device` for the batched engine: BatchNorm folded
     into the preceding convolution (same function in eval mode, fewer kernels per step).
     With `fused` (fp32, AlphaZeroNet / FastOthelloNet) the convolutions run without bias
@@ -180,7 +181,7 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True) -> n
     m = m.to(device=device, dtype=dtype)
     m = m.to(memory_format=torch.channels_last)
     if fused and dtype == torch.float32 and isinstance(m, (AlphaZeroNet, FastOthelloNet)):
-        return FusedInferenceNet(m).eval()
+        return FusedInferenceNet(m, conv=conv).eval()
     return m.eval()
 
 
@@ -209,6 +210,57 @@ class _ConvEpilogue(nn.Module):
         return y
 
 
+class _HipConv3x3(nn.Module):
+    """3x3 conv (Ci = Co in {64, 128}) + bias (+ residual) + ReLU in one fp32 MFMA kernel
+    (csrc/conv.hip); weights re-laid [tap][Co][Ci]."""
+
+    def __init__(self, conv: nn.Conv2d):
+        super().__init__()
+        w = conv.weight.detach()
+        co, ci = w.shape[0], w.shape[1]
+        assert co == ci and co in (64, 128) and w.shape[2:] == (3, 3)
+        self.channels = co
+        self.w9 = nn.Parameter(w.permute(2, 3, 0, 1).reshape(9, co, ci).contiguous(),
+                               requires_grad=False)
+        self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
+
+    def forward(self, x, res=None, relu=True):
+        import az_native as nat
+
+        x = x.contiguous(memory_format=torch.channels_last)
+        if res is not None:
+            res = res.contiguous(memory_format=torch.channels_last)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(self.w9), nat.ptr(self.bias),
+                                         None if res is None else nat.ptr(res), nat.ptr(y),
+                                         x.shape[0], self.channels, int(relu),
+                                         nat.stream_ptr()), "az_conv3x3_gpu")
+        return y
+
+
+class _HipStem(nn.Module):
+    """1 -> C 3x3 stem conv + bias + ReLU on the canonical planes (csrc/conv.hip)."""
+
+    def __init__(self, conv: nn.Conv2d):
+        super().__init__()
+        w = conv.weight.detach()
+        assert w.shape[1] == 1 and w.shape[0] in (64, 128)
+        self.channels = w.shape[0]
+        self.w9 = nn.Parameter(w.reshape(w.shape[0], 9).t().contiguous(), requires_grad=False)
+        self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
+
+    def forward(self, x, res=None, relu=True):
+        import az_native as nat
+
+        planes = x.reshape(x.shape[0], 64).contiguous()
+        y = torch.empty((x.shape[0], self.channels, 8, 8), dtype=torch.float32, device=x.device,
+                        memory_format=torch.channels_last)
+        nat.check(nat.lib.az_conv_stem_gpu(nat.ptr(planes), nat.ptr(self.w9), nat.ptr(self.bias),
+                                           nat.ptr(y), x.shape[0], self.channels,
+                                           nat.stream_ptr()), "az_conv_stem_gpu")
+        return y
+
+
 def _merge_1x1(a: nn.Conv2d, b: nn.Conv2d) -> nn.Conv2d:
     m = nn.Conv2d(a.in_channels, a.out_channels + b.out_channels, 1)
     m.weight = nn.Parameter(torch.cat([a.weight.detach(), b.weight.detach()], 0))
@@ -218,26 +270,31 @@ def _merge_1x1(a: nn.Conv2d, b: nn.Conv2d) -> nn.Conv2d:
 
 class FusedInferenceNet(nn.Module, Inference):
     """Inference-only form of AlphaZeroNet / FastOthelloNet with BatchNorm folded and every
-    conv epilogue fused (same function as the source net in eval mode)."""
+    conv epilogue fused (same function as the source net in eval mode).  conv="hip": the
+    stem and the 3x3 trunk run on the fused MFMA kernels of csrc/conv.hip; conv="miopen":
+    MIOpen convolutions + the az_bias_act_gpu epilogue."""
 
-    def __init__(self, m: nn.Module):
+    def __init__(self, m: nn.Module, conv="hip"):
         super().__init__()
+        self.conv_impl = conv
         self.kind = "az" if isinstance(m, AlphaZeroNet) else "fast"
         self.board_size = m.board_size
         self.softmax = nn.Softmax(dim=-1)
+        C3 = _HipConv3x3 if conv == "hip" else _ConvEpilogue
+        Stem = _HipStem if conv == "hip" else _ConvEpilogue
         if self.kind == "az":
-            self.stem = _ConvEpilogue(m.conv0)
+            self.stem = Stem(m.conv0)
             blocks = list(m.res)
             self.heads = _ConvEpilogue(_merge_1x1(m.pol_conv, m.val_conv))
             self.n_pol = m.pol_conv.out_channels
             self.pol_fc, self.val_fc1, self.val_fc2 = m.pol_fc, m.val_fc1, m.val_fc2
         else:
-            self.stem = _ConvEpilogue(m.initial_conv[0])
+            self.stem = Stem(m.initial_conv[0])
             blocks = [m.res_block]
-            self.tail = _ConvEpilogue(m.conv_add[0])
+            self.tail = C3(m.conv_add[0])
             self.fc_policy, self.fc_value1, self.fc_value2 = m.fc_policy, m.fc_value1, m.fc_value2
-        self.c1 = nn.ModuleList([_ConvEpilogue(b.conv1) for b in blocks])
-        self.c2 = nn.ModuleList([_ConvEpilogue(b.conv2) for b in blocks])
+        self.c1 = nn.ModuleList([C3(b.conv1) for b in blocks])
+        self.c2 = nn.ModuleList([C3(b.conv2) for b in blocks])
 
     def forward(self, x):
         if x.dim() == 3:

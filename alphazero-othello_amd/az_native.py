@@ -98,6 +98,8 @@ SIGNATURES = {
     "az_copy_samples": [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
     "az_clear_samples": [_P, _P],
     "az_bias_act_gpu": [_P, _P, _P, _I64, _I32, _I32, _P],
+    "az_conv3x3_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P],
+    "az_conv_stem_gpu": [_P, _P, _P, _P, _I32, _I32, _P],
 }
 
 

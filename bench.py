@@ -53,8 +53,8 @@ STEP_BYTES = 43            # algorithmic bytes per board step
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4000)
-    ap.add_argument("--warmup", type=int, default=1200)
+    ap.add_argument("--steps", type=int, default=12000)
+    ap.add_argument("--warmup", type=int, default=26000)
     ap.add_argument("--games", type=int, default=1024, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=400)
     ap.add_argument("--net", default="az5x128", choices=["az5x128", "fast"])
@@ -184,7 +184,8 @@ def main():
                          use_graph=not a.no_graph, device=device,
                          sample_capacity=a.games * 130 * 4)
     e = sp.engine
-    sp.reset(start_budget=-1, stagger_steps=max(a.warmup, 1))
+    # stagger slot starts over (at most) one game length so the window sees steady state
+    sp.reset(start_budget=-1, stagger_steps=max(1, min(a.warmup, (a.sims + 1) * 60)))
 
     def barrier():
         torch.cuda.synchronize()
@@ -202,21 +203,10 @@ def main():
     n_new = c_mid["samples"] - c0["samples"]
     allgather_rows = n_new
     if dist is not None:
-        smp = e.samples(c0["samples"], n_new, device=True)
-        cnt = torch.tensor([n_new], device=device, dtype=torch.int64)
-        cnts = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(cnts, cnt)
-        mx = int(max(int(c) for c in cnts))
-        rec = torch.zeros(mx, 2 + 65 + 2, dtype=torch.float64, device=device)
-        if n_new:
-            rec[:n_new, 0] = smp["own"].view(torch.float64)
-            rec[:n_new, 1] = smp["opp"].view(torch.float64)
-            rec[:n_new, 2:67] = smp["pi"].double()
-            rec[:n_new, 67] = smp["z"]
-            rec[:n_new, 68] = smp["player"].double()
-        out = torch.empty(world * mx, rec.shape[1], dtype=rec.dtype, device=device)
-        dist.all_gather_into_tensor(out, rec)
-        allgather_rows = int(sum(int(c) for c in cnts))
+        from dist_replay import allgather_samples
+
+        pooled, counts = allgather_samples(e.samples(c0["samples"], n_new, device=True), device)
+        allgather_rows = int(sum(counts))
     barrier()
     dt = time.perf_counter() - t0
     c1 = e.counters()
@@ -237,7 +227,11 @@ def main():
     plies_all, gtot_all = allst[:, 3].sum(), allst[:, 4].sum()
     t_max = float(allst[:, 5].max())
     plies_per_game = plies_all / gtot_all if gtot_all >= 16 else REF_PLIES_PER_GAME
-    value = moves_all / plies_per_game / t_max
+    if games_all >= 64 * world:
+        value, basis = games_all / t_max, "games completed in the window / window seconds"
+    else:
+        value = moves_all / plies_per_game / t_max
+        basis = "moves completed in the window / plies per game / window seconds"
 
     result = {
         "metric": "self-play games/sec (whole node), 8x8 Othello @ 400 MCTS sims/move",
@@ -251,7 +245,9 @@ def main():
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
                    "parallelism": f"dp{world} (independent games per GPU)",
                    "hip_graph": sp.graph is not None},
-        "detail": {"moves": int(moves_all), "games_finished_in_window": int(games_all),
+        "value_basis": basis,
+        "detail": {"moves": int(moves_all),
+                   "game_equivalents_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),
                    "simulations": int(sims_all), "plies_per_game": round(float(plies_per_game), 2),
                    "sims_per_s": round(float(sims_all / t_max), 1),
                    "window_s": round(t_max, 3), "allgather_rows": allgather_rows,

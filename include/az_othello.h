@@ -238,6 +238,20 @@ int az_clear_samples(az_engine* eng, void* stream);
 int az_bias_act_gpu(float* y, const float* bias, const float* res, int64_t n,
                     int32_t channels, int32_t relu, void* stream);
 
+/* 3x3 convolution, padding 1, over n_boards 8x8 boards, Ci = Co = channels (64 or 128),
+ * fp32 MFMA, fused epilogue: y = act(conv(x, w) + bias (+ res)).  x, res, y: NHWC float
+ * [n_boards, 8, 8, C]; w9: [9 taps (ky*3+kx)][Co][Ci]; res may be NULL; x != y.  Replaces
+ * ResidualBlock.conv1/conv2 + BatchNorm (folded) + skip + ReLU (Models.py:72-90) and
+ * FastOthelloNet.conv_add (Models.py:119-121). */
+int az_conv3x3_gpu(const float* x, const float* w9, const float* bias, const float* res,
+                   float* y, int32_t n_boards, int32_t channels, int32_t relu, void* stream);
+
+/* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
+ * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,
+ * 186-187). */
+int az_conv_stem_gpu(const float* planes, const float* w9, const float* bias, float* y,
+                     int32_t n_boards, int32_t channels, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

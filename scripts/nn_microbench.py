@@ -26,6 +26,10 @@ def timeit(fn, x, reps=50):
     return e0.elapsed_time(e1) / reps
 
 
+def plain_p(net, x):
+    return torch.softmax(net(x.view(-1, 1, 8, 8))[0], -1)
+
+
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     dev = torch.device("cuda")
@@ -39,8 +43,12 @@ def main():
             r["plain_ms"] = timeit(lambda t: plain(t.view(-1, 1, 8, 8)), x)
             fold = inference_copy(net, dev, fused=False)
             r["folded_cl_ms"] = timeit(fold.evaluate_planes, x)
-            fused = inference_copy(net, dev, fused=True)
+            fused = inference_copy(net, dev, fused=True, conv="miopen")
             r["fused_ms"] = timeit(fused.evaluate_planes, x)
+            hip = inference_copy(net, dev, fused=True, conv="hip")
+            r["hipconv_ms"] = timeit(hip.evaluate_planes, x)
+            c2 = hip.evaluate_planes(x)
+            r["max_abs_prior_diff_hipconv"] = float((c2[0] - plain_p(plain, x)).abs().max())
             c = fused.evaluate_planes(x)
             b0 = fold.evaluate_planes(x)
             r["max_abs_prior_diff_fused"] = float((c[0] - b0[0]).abs().max())
@@ -48,7 +56,7 @@ def main():
             torch.backends.cudnn.benchmark = True
             fold2 = inference_copy(net, dev, fused=False)
             r["folded_cl_find_ms"] = timeit(fold2.evaluate_planes, x)
-            fused2 = inference_copy(net, dev, fused=True)
+            fused2 = inference_copy(net, dev, fused=True, conv="miopen")
             r["fused_find_ms"] = timeit(fused2.evaluate_planes, x)
             torch.backends.cudnn.benchmark = False
             h = inference_copy(net, dev, torch.float16)
@@ -58,6 +66,7 @@ def main():
         flops = {"az5x128": 189.0e6, "fast": 15.29e6}[name] * B
         r["tflops_folded"] = flops / (r["folded_cl_ms"] * 1e-3) / 1e12
         r["tflops_fused"] = flops / (r["fused_ms"] * 1e-3) / 1e12
+        r["tflops_hipconv"] = flops / (r["hipconv_ms"] * 1e-3) / 1e12
         out[name] = r
     print(json.dumps(out))
 

@@ -1,0 +1,75 @@
+"""The N>1 path on CPU: world_size-2 gloo process group running the per-generation replay
+all-gather (dist_replay.allgather_samples) and the best-net broadcast, bit-exact."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rows(rank, n):
+    rng = np.random.default_rng(rank)
+    return {"own": rng.integers(0, 2**63, n, dtype=np.int64).astype(np.uint64) | np.uint64(1 << 63),
+            "opp": rng.integers(0, 2**63, n, dtype=np.int64).astype(np.uint64),
+            "pi": rng.random((n, 65)).astype(np.float32),
+            "z": rng.standard_normal(n),
+            "player": rng.choice([-1, 1], n).astype(np.int8)}
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "alphazero-othello_amd"))
+    from dist_replay import allgather_samples, broadcast_state_dict
+    from Models import FastOthelloNet
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    counts = [5, 0, 3][:world]
+    got, cnts = allgather_samples(_rows(rank, counts[rank]), "cpu")
+    torch.manual_seed(rank)
+    net = FastOthelloNet(8, 65)
+    broadcast_state_dict(net, src=0)
+    w = float(net.fc_value2.weight.sum())
+    q.put((rank, cnts, {k: v.numpy() for k, v in got.items()}, w))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_replay_allgather_world2_bit_exact():
+    res = _run(2)
+    want = [_rows(0, 5), _rows(1, 0)]
+    for rank, cnts, got, w in res:
+        assert cnts == [5, 0]
+        for k in ("own", "opp", "pi", "z", "player"):
+            exp = np.concatenate([want[0][k], want[1][k]])
+            g = got[k]
+            if k in ("own", "opp"):
+                g = g.view(np.uint64)
+            assert np.array_equal(g, exp), k
+    assert res[0][3] == res[1][3]  # broadcast weights identical on every rank
