@@ -91,6 +91,10 @@ SIGNATURES = {
     "az_root_policy": [_P, _I32, _D, _D, _P, _P, _P, _P],
     "az_make_move": [_P, _I32, _I32, _P],
     "az_counters": [_P, _P, _P],
+    "az_set_roots": [_P, _P, _P, _P, _P, _I32, _P],
+    "az_begin_search_slots": [_P, _P, _I32, _I32, _P],
+    "az_root_stats": [_P, _P, _P, _P],
+    "az_reroot_slots": [_P, _P, _P, _P],
     "az_game_info": [_P, _P, _P, _P, _P, _P, _P, _P],
     "az_export_tree": [_P, _I32, _I32] + [_P] * 13,
     "az_export_trajectory": [_P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
@@ -100,6 +104,7 @@ SIGNATURES = {
     "az_bias_act_gpu": [_P, _P, _P, _I64, _I32, _I32, _P],
     "az_conv3x3_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P],
     "az_conv_stem_gpu": [_P, _P, _P, _P, _I32, _I32, _P],
+    "az_conv3x3_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
 }
 
 

@@ -123,8 +123,12 @@ AZ_HD void play(uint64_t own, uint64_t opp, int act, uint64_t cap, uint64_t* now
 
 // Terminal flags / value of a position (side to move = own): reference
 // get_value_and_terminated (envs/othello.py:435-454) evaluated for the side to move.
+// The opponent's full legal-mask fill runs only when no cheap proof exists: a full board
+// or a side without stones ends the game outright (neither side can bound anything), so a
+// wavefront skips the divergent second fill unless one of its lanes holds a real pass.
 AZ_HD int terminal_flags(uint64_t own, uint64_t opp, uint64_t lg) {
   if (lg) return 0;
+  if ((own | opp) == ~0ull || own == 0 || opp == 0) return kFlagNoPlace | kFlagTerminal;
   return legal(opp, own) ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
 }
 

@@ -21,27 +21,26 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kBoards = 2;  // boards per workgroup
-constexpr int kThreads = 256;
-
-template <int C>
+// Tiling: a workgroup of WAVES waves owns BOARDS boards (M = 64*BOARDS rows) x all C
+// output channels; each wave a TM x TN block of 32x32 MFMA tiles.
+template <int C_, int BOARDS_, int WAVES_, int TM_, int TN_>
 struct Geo {
-  static constexpr int S = C + 4;                  // LDS floats per position (padded)
-  static constexpr int TM = C == 128 ? 2 : 1;      // 32-row MFMA tiles per wave
-  static constexpr int TN = 2;                     // 32-col MFMA tiles per wave
-  static constexpr int WM = 32 * TM;               // rows per wave
-  static constexpr int WN = 32 * TN;               // cols per wave
-  static constexpr int WAVES_N = C / WN;           // waves along N
-  static_assert((kBoards * 64 / WM) * WAVES_N == 4, "4 waves per workgroup");
+  static constexpr int C = C_, BOARDS = BOARDS_, WAVES = WAVES_, TM = TM_, TN = TN_;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int S = C + 4;       // LDS floats per position (padded: conflict-free rows)
+  static constexpr int WM = 32 * TM;    // rows per wave
+  static constexpr int WN = 32 * TN;    // cols per wave
+  static constexpr int WAVES_N = C / WN;
+  static_assert((BOARDS * 64 / WM) * WAVES_N == WAVES, "tiling must cover the workgroup");
 };
 
-template <int C, bool RES, bool RELU>
-__global__ __launch_bounds__(kThreads, 2) void k_conv3x3(const float* __restrict__ x,
-                                                         const float* __restrict__ w,
-                                                         const float* __restrict__ bias,
-                                                         const float* __restrict__ res,
-                                                         float* __restrict__ y, int n_boards) {
-  using G = Geo<C>;
+template <class G, bool RES, bool RELU>
+__global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict__ x,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ res,
+                                                        float* __restrict__ y, int n_boards) {
+  constexpr int C = G::C, kBoards = G::BOARDS, kThreads = G::THREADS;
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   const int tid = threadIdx.x;
@@ -193,29 +192,62 @@ __global__ __launch_bounds__(256) void k_conv_stem(const float* __restrict__ pla
   }
 }
 
-template <int C>
+template <class G>
 int launch_conv(const float* x, const float* w, const float* bias, const float* res, float* y,
                 int n_boards, int relu, hipStream_t s) {
-  const unsigned grid = (unsigned)((n_boards + kBoards - 1) / kBoards);
-  const size_t lds = (size_t)kBoards * 64 * Geo<C>::S * sizeof(float);
+  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  const size_t lds = (size_t)G::BOARDS * 64 * G::S * sizeof(float);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in once per kernel
   if (!attr_set) {
-    const void* ks[] = {(const void*)k_conv3x3<C, true, true>, (const void*)k_conv3x3<C, true, false>,
-                        (const void*)k_conv3x3<C, false, true>, (const void*)k_conv3x3<C, false, false>};
+    const void* ks[] = {(const void*)k_conv3x3<G, true, true>, (const void*)k_conv3x3<G, true, false>,
+                        (const void*)k_conv3x3<G, false, true>, (const void*)k_conv3x3<G, false, false>};
     for (const void* k : ks)
       AZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_set = true;
   }
+  const dim3 blk(G::THREADS);
   if (res && relu)
-    hipLaunchKernelGGL((k_conv3x3<C, true, true>), dim3(grid), dim3(kThreads), lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
   else if (res)
-    hipLaunchKernelGGL((k_conv3x3<C, true, false>), dim3(grid), dim3(kThreads), lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
   else if (relu)
-    hipLaunchKernelGGL((k_conv3x3<C, false, true>), dim3(grid), dim3(kThreads), lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
   else
-    hipLaunchKernelGGL((k_conv3x3<C, false, false>), dim3(grid), dim3(kThreads), lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
+}
+
+// tiling candidates (C, boards, waves, TM, TN); index 0 of each C is the default, picked
+// by scripts/conv_bench.py on MI355X (B = 1024: C=128 176 us vs MIOpen's 175 us for the
+// bare convolution; C=64 51 us vs 59 us)
+using G128_0 = Geo<128, 2, 8, 1, 2>;
+using G128_1 = Geo<128, 1, 4, 1, 2>;
+using G128_2 = Geo<128, 4, 8, 2, 2>;
+using G128_3 = Geo<128, 2, 4, 2, 2>;
+using G128_4 = Geo<128, 1, 2, 2, 2>;
+using G64_0 = Geo<64, 1, 2, 1, 2>;
+using G64_1 = Geo<64, 2, 4, 1, 2>;
+using G64_2 = Geo<64, 4, 4, 2, 2>;
+
+int launch_cfg(int cfg, const float* x, const float* w, const float* bias, const float* res,
+               float* y, int n_boards, int channels, int relu, hipStream_t s) {
+  if (channels == 128) {
+    switch (cfg) {
+      case 0: return launch_conv<G128_0>(x, w, bias, res, y, n_boards, relu, s);
+      case 1: return launch_conv<G128_1>(x, w, bias, res, y, n_boards, relu, s);
+      case 2: return launch_conv<G128_2>(x, w, bias, res, y, n_boards, relu, s);
+      case 3: return launch_conv<G128_3>(x, w, bias, res, y, n_boards, relu, s);
+      case 4: return launch_conv<G128_4>(x, w, bias, res, y, n_boards, relu, s);
+    }
+  } else if (channels == 64) {
+    switch (cfg) {
+      case 0: return launch_conv<G64_0>(x, w, bias, res, y, n_boards, relu, s);
+      case 1: return launch_conv<G64_1>(x, w, bias, res, y, n_boards, relu, s);
+      case 2: return launch_conv<G64_2>(x, w, bias, res, y, n_boards, relu, s);
+    }
+  }
+  return azc::set_error(AZ_ERR_ARG, "az_conv3x3: no tiling %d for %d channels", cfg, channels);
 }
 
 }  // namespace
@@ -229,11 +261,19 @@ extern "C" int az_conv3x3_gpu(const float* x, const float* w9, const float* bias
              "az_conv3x3_gpu: null buffer or in-place call");
   AZ_REQUIRE(((uintptr_t)x | (uintptr_t)w9 | (uintptr_t)bias) % 16 == 0, AZ_ERR_ARG,
              "az_conv3x3_gpu: buffers must be 16-byte aligned");
-  hipStream_t s = azc::as_stream(stream);
-  if (channels == 128) return launch_conv<128>(x, w9, bias, res, y, n_boards, relu, s);
-  if (channels == 64) return launch_conv<64>(x, w9, bias, res, y, n_boards, relu, s);
-  return azc::set_error(AZ_ERR_ARG, "az_conv3x3_gpu: channels must be 64 or 128, got %d",
-                        channels);
+  AZ_REQUIRE(channels == 64 || channels == 128, AZ_ERR_ARG,
+             "az_conv3x3_gpu: channels must be 64 or 128, got %d", channels);
+  return launch_cfg(0, x, w9, bias, res, y, n_boards, channels, relu, azc::as_stream(stream));
+}
+
+// same op with an explicit tiling candidate (benchmarking the tile space)
+extern "C" int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* bias,
+                                  const float* res, float* y, int32_t n_boards,
+                                  int32_t channels, int32_t relu, int32_t cfg, void* stream) {
+  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_cfg_gpu: n_boards < 0");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(x && w9 && bias && y && x != y, AZ_ERR_ARG, "az_conv3x3_cfg_gpu: bad buffers");
+  return launch_cfg(cfg, x, w9, bias, res, y, n_boards, channels, relu, azc::as_stream(stream));
 }
 
 extern "C" int az_conv_stem_gpu(const float* planes, const float* w9, const float* bias,

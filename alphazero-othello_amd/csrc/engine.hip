@@ -355,7 +355,7 @@ __device__ double rollout(const Params& p, int g, uint64_t own, uint64_t opp) {
     own = no;
     opp = np_;
     side = -side;
-    if (!azb::legal(own, opp) && !azb::legal(opp, own)) {
+    if (azb::terminal_flags(own, opp, azb::legal(own, opp)) & azb::kFlagTerminal) {
       const int d = (azb::popc(own) - azb::popc(opp)) * side;
       return d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0);
     }
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
       uint64_t co, cp;
       azb::play(own, opp, a, lg ? azb::flips(own, opp, a) : 0ull, &co, &cp);
       const uint64_t clg = azb::legal(co, cp);
-      const bool term = clg == 0 && azb::legal(cp, co) == 0;
+      const bool term = (azb::terminal_flags(co, cp, clg) & azb::kFlagTerminal) != 0;
       const int d = azb::popc(co) - azb::popc(cp);
       const int64_t c = nidx(p, half, g, fc + ci);
       p.a.own[c] = co;
@@ -941,6 +941,95 @@ __global__ __launch_bounds__(kMoveBlock) void k_reroot(Params p, int g, int acti
   }
 }
 
+// ---- batched host-driven control (arena evaluation: many independent searches) -------
+
+__global__ void k_set_roots(Params p, const int32_t* slots, const uint64_t* own,
+                            const uint64_t* opp, const int32_t* player, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int g = slots[i];
+  if (g < 0 || g >= p.G) return;
+  p.g.half[g] = 0;
+  init_root(p, g, 0, own[i], opp[i]);
+  p.g.n_nodes[g] = 1;
+  p.g.root_player[g] = player[i];
+  p.g.leaf[g] = -1;
+  p.g.sims_done[g] = 0;
+  p.g.sims_target[g] = 0;
+  p.g.status[g] = kSearchDone;
+}
+
+__global__ void k_begin_slots(Params p, const int32_t* slots, int n, int sims) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int g = slots[i];
+  if (g < 0 || g >= p.G) return;
+  p.g.sims_done[g] = 0;
+  p.g.sims_target[g] = sims;
+  p.g.leaf[g] = -1;
+  p.g.status[g] = kActive;
+}
+
+// child visit counts (int32 [G, 65]) and root W/N of every slot: one wave per slot
+__global__ __launch_bounds__(kSelBlock) void k_root_stats(Params p, int32_t* counts,
+                                                          double* vroot) {
+  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+  if (g >= p.G) return;
+  const int lane = lane_id();
+  const int half = p.g.half[g];
+  const int64_t r = nidx(p, half, g, 0);
+  int32_t* row = counts + (int64_t)g * 65;
+  row[lane] = 0;
+  if (lane == 0) row[64] = 0;
+  const int nc = (p.a.flags[r] & kExpanded) ? p.a.nchild[r] : 0, fc = p.a.first[r];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (lane < nc) {
+    const int64_t c = nidx(p, half, g, fc + lane);
+    row[p.a.action[c]] = p.a.N[c];
+  }
+  if (lane == 0) {
+    const int n = p.a.N[r];
+    vroot[g] = n == 0 ? 0.0 : p.a.W[r] / (double)n;
+  }
+}
+
+// re-root every slot with actions[g] >= 0 (MCTS.make_move on many trees at once);
+// found[g] = child node or -1 (KeyError / no tree); one workgroup per slot
+__global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(Params p, const int32_t* actions,
+                                                             int32_t* found) {
+  extern __shared__ int32_t map[];
+  __shared__ int s_child;
+  for (int g = blockIdx.x; g < p.G; g += gridDim.x) {
+    const int action = actions[g];
+    if (action < 0) {
+      if (threadIdx.x == 0) found[g] = -1;
+      continue;
+    }
+    const int half = p.g.half[g];
+    if (threadIdx.x == 0) {
+      const int64_t r = nidx(p, half, g, 0);
+      const int nc = (p.a.flags[r] & kExpanded) ? p.a.nchild[r] : 0, fc = p.a.first[r];
+      int child = -1;
+      for (int j = 0; j < nc; ++j)
+        if (p.a.action[nidx(p, half, g, fc + j)] == action) child = fc + j;
+      s_child = child;
+      found[g] = child;
+    }
+    __syncthreads();
+    if (s_child >= 0) {
+      const int player = p.g.root_player[g];
+      compact(p, g, s_child, map);
+      if (threadIdx.x == 0) {
+        p.g.root_player[g] = -player;
+        p.g.sims_done[g] = 0;
+        p.g.sims_target[g] = 0;
+        p.g.status[g] = kSearchDone;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ====================================================================================
@@ -952,6 +1041,14 @@ struct az_engine {
   std::vector<void*> allocs;
   int32_t* d_result = nullptr;
   char* d_scratch = nullptr;  // 1 KiB: az_root_policy outputs
+  // batched host-driven control buffers ([G] each, counts [G, 65])
+  int32_t* d_slots = nullptr;
+  int32_t* d_ivec = nullptr;
+  int32_t* d_found = nullptr;
+  int32_t* d_counts = nullptr;
+  double* d_vroot = nullptr;
+  uint64_t* d_own = nullptr;
+  uint64_t* d_opp = nullptr;
   size_t lds_move = 0;
 };
 
@@ -1089,6 +1186,13 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   p.inj_u = uni;
   chk(dalloc(e, &e->d_result, 4));
   chk(dalloc(e, &e->d_scratch, 1024));
+  chk(dalloc(e, &e->d_slots, G));
+  chk(dalloc(e, &e->d_ivec, G));
+  chk(dalloc(e, &e->d_found, G));
+  chk(dalloc(e, &e->d_counts, G * 65));
+  chk(dalloc(e, &e->d_vroot, G));
+  chk(dalloc(e, &e->d_own, G));
+  chk(dalloc(e, &e->d_opp, G));
   if (rc != AZ_OK) {
     free_all(e);
     delete e;
@@ -1098,6 +1202,8 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   if (hipFuncSetAttribute((const void*)k_move, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_reroot, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_reroot_slots, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess) {
     (void)hipGetLastError();
   }
@@ -1246,6 +1352,71 @@ int az_make_move(az_engine* e, int32_t slot, int32_t action, void* stream) {
   AZ_HIP(hipStreamSynchronize(s));
   // KeyError in the reference (MCTS_model.py:214)
   AZ_REQUIRE(child >= 0, AZ_ERR_STATE, "%d", action);
+  return AZ_OK;
+}
+
+int az_set_roots(az_engine* e, const int32_t* slots, const uint64_t* own, const uint64_t* opp,
+                 const int32_t* player, int32_t n, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(n >= 0 && n <= e->p.G, AZ_ERR_ARG, "az_set_roots: n out of range");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(slots && own && opp && player, AZ_ERR_ARG, "az_set_roots: null buffer");
+  for (int i = 0; i < n; ++i) {
+    AZ_REQUIRE(slots[i] >= 0 && slots[i] < e->p.G, AZ_ERR_ARG, "slot %d out of range", slots[i]);
+    AZ_REQUIRE((own[i] & opp[i]) == 0, AZ_ERR_ARG, "own and opp overlap (slot %d)", slots[i]);
+    AZ_REQUIRE(player[i] == 1 || player[i] == -1, AZ_ERR_ARG, "player must be +1 or -1");
+  }
+  hipStream_t s = azc::as_stream(stream);
+  AZ_HIP(hipMemcpyAsync(e->d_slots, slots, n * 4, hipMemcpyHostToDevice, s));
+  AZ_HIP(hipMemcpyAsync(e->d_own, own, n * 8, hipMemcpyHostToDevice, s));
+  AZ_HIP(hipMemcpyAsync(e->d_opp, opp, n * 8, hipMemcpyHostToDevice, s));
+  AZ_HIP(hipMemcpyAsync(e->d_ivec, player, n * 4, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_set_roots, dim3((n + 255) / 256), dim3(256), 0, s, e->p, e->d_slots,
+                     e->d_own, e->d_opp, e->d_ivec, (int)n);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_begin_search_slots(az_engine* e, const int32_t* slots, int32_t n,
+                          int32_t num_simulations, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(n >= 0 && n <= e->p.G && num_simulations >= 0, AZ_ERR_ARG,
+             "az_begin_search_slots: bad n / num_simulations");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(slots, AZ_ERR_ARG, "az_begin_search_slots: null slots");
+  hipStream_t s = azc::as_stream(stream);
+  AZ_HIP(hipMemcpyAsync(e->d_slots, slots, n * 4, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_begin_slots, dim3((n + 255) / 256), dim3(256), 0, s, e->p, e->d_slots,
+                     (int)n, (int)num_simulations);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_root_stats(az_engine* e, int32_t* counts, double* vroot, void* stream) {
+  AZ_REQUIRE(e && counts, AZ_ERR_ARG, "az_root_stats: null argument");
+  hipStream_t s = azc::as_stream(stream);
+  hipLaunchKernelGGL(k_root_stats, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, e->d_counts,
+                     e->d_vroot);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipMemcpyAsync(counts, e->d_counts, (size_t)e->p.G * 65 * 4, hipMemcpyDeviceToHost, s));
+  if (vroot)
+    AZ_HIP(hipMemcpyAsync(vroot, e->d_vroot, (size_t)e->p.G * 8, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  return AZ_OK;
+}
+
+int az_reroot_slots(az_engine* e, const int32_t* actions, int32_t* found, void* stream) {
+  AZ_REQUIRE(e && actions && found, AZ_ERR_ARG, "az_reroot_slots: null argument");
+  hipStream_t s = azc::as_stream(stream);
+  AZ_HIP(hipMemcpyAsync(e->d_ivec, actions, (size_t)e->p.G * 4, hipMemcpyHostToDevice, s));
+  const int blocks = e->p.G < 256 ? e->p.G : 256;
+  hipLaunchKernelGGL(k_reroot_slots, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->p,
+                     e->d_ivec, e->d_found);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipMemcpyAsync(found, e->d_found, (size_t)e->p.G * 4, hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
   return AZ_OK;
 }
 

@@ -135,6 +135,35 @@ class Engine:
         nat.check(nat.lib.az_make_move(self.h, int(slot), int(action), self._s()),
                   "az_make_move")
 
+    # ---- batched host-driven control (arena) ----------------------------------------
+    def set_roots(self, slots, own, opp, player):
+        slots = np.ascontiguousarray(slots, np.int32)
+        own = np.ascontiguousarray(own, np.uint64)
+        opp = np.ascontiguousarray(opp, np.uint64)
+        player = np.ascontiguousarray(player, np.int32)
+        nat.check(nat.lib.az_set_roots(self.h, nat.ptr(slots), nat.ptr(own), nat.ptr(opp),
+                                       nat.ptr(player), len(slots), self._s()), "az_set_roots")
+
+    def begin_search_slots(self, slots, sims):
+        slots = np.ascontiguousarray(slots, np.int32)
+        nat.check(nat.lib.az_begin_search_slots(self.h, nat.ptr(slots), len(slots), int(sims),
+                                                self._s()), "az_begin_search_slots")
+
+    def root_stats(self):
+        counts = np.zeros((self.G, 65), np.int32)
+        vroot = np.zeros(self.G, np.float64)
+        nat.check(nat.lib.az_root_stats(self.h, nat.ptr(counts), nat.ptr(vroot), self._s()),
+                  "az_root_stats")
+        return counts, vroot
+
+    def reroot_slots(self, actions):
+        actions = np.ascontiguousarray(actions, np.int32)
+        assert actions.shape == (self.G,)
+        found = np.zeros(self.G, np.int32)
+        nat.check(nat.lib.az_reroot_slots(self.h, nat.ptr(actions), nat.ptr(found), self._s()),
+                  "az_reroot_slots")
+        return found
+
     def counters(self):
         out = np.zeros(8, np.int64)
         nat.check(nat.lib.az_counters(self.h, nat.ptr(out), self._s()), "az_counters")

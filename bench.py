@@ -55,16 +55,27 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=12000)
     ap.add_argument("--warmup", type=int, default=26000)
-    ap.add_argument("--games", type=int, default=1024, help="concurrent games per GPU")
-    ap.add_argument("--sims", type=int, default=400)
-    ap.add_argument("--net", default="az5x128", choices=["az5x128", "fast"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
+                    help="BASELINE.json configs: c2 = 4096 games x 100 sims FastOthelloNet; "
+                         "c3 = 1024 games x 400 sims AlphaZeroNet(5x128) fp32 (the metric's "
+                         "config, default); c5 = c3 + fused D4 augmentation + fp16 inference")
+    ap.add_argument("--games", type=int, default=None, help="concurrent games per GPU")
+    ap.add_argument("--sims", type=int, default=None)
+    ap.add_argument("--net", default=None, choices=["az5x128", "fast"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-kernel", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "oth_step_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    preset = {"c2": (4096, 100, "fast", False, "fp32"), "c3": (1024, 400, "az5x128", False, "fp32"),
+              "c5": (1024, 400, "az5x128", True, "fp16")}[a.workload]
+    a.games = a.games or preset[0]
+    a.sims = a.sims or preset[1]
+    a.net = a.net or preset[2]
+    a.d4, a.precision = preset[3], preset[4]
+    return a
 
 
 def make_net(kind):
@@ -168,20 +179,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AZ_BENCH_REHEARSE=1: every rank on cuda:0 with gloo collectives (rehearses the N>1
+    # path on a one-GPU box); otherwise one GPU per rank and RCCL ("nccl")
+    rehearse = os.environ.get("AZ_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    coll_device = torch.device("cpu") if rehearse else device
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from engine import BatchedSelfPlay
 
     net = make_net(a.net)
     args = dict(SELFPLAY_ARGS, num_simulations=a.sims)
     sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
-                         use_graph=not a.no_graph, device=device,
+                         use_graph=not a.no_graph, device=device, d4_augment=a.d4,
+                         dtype=torch.float16 if a.precision == "fp16" else torch.float32,
                          sample_capacity=a.games * 130 * 4)
     e = sp.engine
     # stagger slot starts over (at most) one game length so the window sees steady state
@@ -205,7 +226,8 @@ def main():
     if dist is not None:
         from dist_replay import allgather_samples
 
-        pooled, counts = allgather_samples(e.samples(c0["samples"], n_new, device=True), device)
+        pooled, counts = allgather_samples(e.samples(c0["samples"], n_new, device=not rehearse),
+                                           coll_device)
         allgather_rows = int(sum(counts))
     barrier()
     dt = time.perf_counter() - t0
@@ -216,7 +238,7 @@ def main():
     plies_total = c1["samples"]
     games_total = c1["games_finished"]
     stats = torch.tensor([moves, games_done, sims, plies_total, games_total, dt],
-                         dtype=torch.float64, device=device)
+                         dtype=torch.float64, device=coll_device)
     if dist is not None:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)
@@ -234,14 +256,19 @@ def main():
         basis = "moves completed in the window / plies per game / window seconds"
 
     result = {
-        "metric": "self-play games/sec (whole node), 8x8 Othello @ 400 MCTS sims/move",
+        "metric": f"self-play games/sec (whole node), 8x8 Othello @ {a.sims} MCTS sims/move",
         "value": round(float(value), 4), "unit": "games/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(t_max * 1000.0 / a.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (net), int64 bitboards",
+        "scaling": "weak", "vs_baseline": None, "dtype": f"{a.precision} (net), int64 bitboards",
         "data": "synthetic: self-play from the initial position, random-init net weights",
-        "config": {"workload": "configs[2]: 8x8 Othello, 400 sims/move, AlphaZeroNet(5x128) "
-                               "random init, leaf batch = concurrent games",
+        "config": {"workload": {"c3": "configs[2]: 8x8 Othello, 400 sims/move, AlphaZeroNet(5x128) "
+                                      "random init fp32, leaf batch 1024 = concurrent games",
+                                "c2": "configs[1]: 8x8 Othello, 4096 concurrent games, 100 sims/move, "
+                                      "FastOthelloNet random init fp32",
+                                "c5": "configs[4]: configs[2] + fused D4 symmetry per leaf + fp16 "
+                                      "net inference"}[a.workload],
+                   "d4_augment": a.d4,
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
                    "parallelism": f"dp{world} (independent games per GPU)",
                    "hip_graph": sp.graph is not None},

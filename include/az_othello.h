@@ -194,6 +194,22 @@ int az_root_policy(az_engine* eng, int32_t slot, double temp, double u_tie, floa
  * (KeyError in the reference).  Synchronous. */
 int az_make_move(az_engine* eng, int32_t slot, int32_t action, void* stream);
 
+/* ---- batched host-driven control (many independent searches, e.g. arena matches,
+ * eval.py:46-178).  Host arrays; synchronous. ---- */
+/* roots of n slots at arbitrary positions (as az_set_root, one call). */
+int az_set_roots(az_engine* eng, const int32_t* slots, const uint64_t* own, const uint64_t* opp,
+                 const int32_t* player, int32_t n, void* stream);
+/* start a search of num_simulations on each listed slot. */
+int az_begin_search_slots(az_engine* eng, const int32_t* slots, int32_t n,
+                          int32_t num_simulations, void* stream);
+/* child visit counts int32 [G, 65] (the `counts` of MCTS_model.py:244-247) and root W/N
+ * double [G] (vroot may be NULL) of every slot. */
+int az_root_stats(az_engine* eng, int32_t* counts, double* vroot, void* stream);
+/* MCTS.make_move on every slot with actions[g] >= 0 (int32 [G]); found[g] = the child
+ * that became the root, or -1 when the root has no such child (KeyError,
+ * MCTS_model.py:214) or actions[g] < 0 — that slot's tree is then unchanged. */
+int az_reroot_slots(az_engine* eng, const int32_t* actions, int32_t* found, void* stream);
+
 /* counters: [games_started, games_finished, samples, samples_dropped, arena_overflows,
  * steps, simulations, moves].  Synchronous. */
 int az_counters(az_engine* eng, int64_t* out8, void* stream);
@@ -245,6 +261,12 @@ int az_bias_act_gpu(float* y, const float* bias, const float* res, int64_t n,
  * FastOthelloNet.conv_add (Models.py:119-121). */
 int az_conv3x3_gpu(const float* x, const float* w9, const float* bias, const float* res,
                    float* y, int32_t n_boards, int32_t channels, int32_t relu, void* stream);
+
+/* the same convolution with an explicit tiling candidate `cfg` (benchmarking; 0 = the
+ * default tiling used by az_conv3x3_gpu). */
+int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* bias, const float* res,
+                       float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t cfg,
+                       void* stream);
 
 /* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
  * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,

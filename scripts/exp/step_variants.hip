@@ -149,11 +149,100 @@ __global__ __launch_bounds__(256) void v9(const uint64_t* own, const uint64_t* o
   if (i < n) { azb::Step s = azb::step(own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
 }
 
+// --- v10: no terminal check; v11: cooperative terminal check; v12: make-move only
+namespace y {
+using namespace azb;
+__device__ __forceinline__ void step_core(uint64_t own, uint64_t opp, int act, uint64_t& no, uint64_t& np,
+                                          int& flags, bool& illegal) {
+  flags = 0; illegal = false;
+  if (act == kPass) { no = opp; np = own; flags = kFlagPassed; return; }
+  const bool in_range = (unsigned)act < 64u;
+  const int sq = act & 63;
+  const uint64_t nb = 1ull << sq;
+  const uint64_t cap = in_range ? flips(own, opp, sq) : 0ull;
+  if (!in_range || cap == 0ull || (nb & (own | opp))) { no = own; np = opp; illegal = true; return; }
+  no = opp ^ cap; np = (own | nb) ^ cap;
+}
+// one direction of the legal-move fill (dumb7 with doubling), direction d in 0..7
+__device__ __forceinline__ uint64_t dir_moves(uint64_t P, uint64_t O, int d) {
+  const uint64_t empty = ~(P | O);
+  const uint64_t inner = O & kInner;
+  uint64_t M, f, mm;
+  int s; bool left;
+  switch (d & 3) { case 0: s = 1; M = inner; break; case 1: s = 8; M = O; break;
+                   case 2: s = 7; M = inner; break; default: s = 9; M = inner; break; }
+  left = d >= 4;
+  if (left) {
+    f = M & (P << s); f |= M & (f << s); mm = M & (M << s);
+    f |= mm & (f << (2 * s)); f |= mm & (f << (2 * s));
+    return (f << s) & empty;
+  } else {
+    f = M & (P >> s); f |= M & (f >> s); mm = M & (M >> s);
+    f |= mm & (f >> (2 * s)); f |= mm & (f >> (2 * s));
+    return (f >> s) & empty;
+  }
+}
+}  // namespace y
+
+__global__ __launch_bounds__(256) void v10(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS {
+    uint64_t no, np; int flags; bool ill;
+    y::step_core(own[i], opp[i], act[i], no, np, flags, ill);
+    uint64_t lg = ill ? 0 : azb::legal(no, np);
+    oo[i] = no; po[i] = np; lo[i] = lg;
+    so[i] = azb::pack_status(ill ? azb::kFlagIllegal : flags | (lg ? 0 : azb::kFlagNoPlace), ill ? 0 : azb::popc(no) - azb::popc(np));
+  }
+}
+__global__ __launch_bounds__(256) void v11(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t n_pad = (n + 255) / 256 * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    uint64_t no = 0, np = 0; int flags = 0; bool ill = true;
+    if (live) y::step_core(own[i], opp[i], act[i], no, np, flags, ill);
+    const uint64_t lg = ill ? 0 : azb::legal(no, np);
+    // terminal check for the rare lanes with no placement: 8 lanes per position, one
+    // direction each (opp' moving against own'), up to 8 positions per pass
+    uint64_t need = __ballot(!ill && lg == 0);
+    bool other = false;
+    while (need) {
+      // j-th needed lane for group j = lane / 8
+      const int grp = lane >> 3;
+      uint64_t mm = need; for (int j = 0; j < grp && mm; ++j) mm &= mm - 1;
+      const int src = mm ? __builtin_ctzll(mm) : -1;
+      const uint64_t P = __shfl(np, src < 0 ? 0 : src, 64), O = __shfl(no, src < 0 ? 0 : src, 64);
+      const uint64_t mv = src < 0 ? 0 : y::dir_moves(P, O, lane & 7);
+      const uint64_t got = __ballot(mv != 0);
+      // owner lanes read their group's byte
+      uint64_t mm2 = need; int k = 0;
+      for (; k < 8 && mm2; ++k) { const int l = __builtin_ctzll(mm2); if (l == lane) other = ((got >> (8 * k)) & 0xFF) != 0; mm2 &= mm2 - 1; }
+      // drop the processed lanes (the first 8 set bits)
+      for (int j = 0; j < 8 && need; ++j) need &= need - 1;
+    }
+    if (live) {
+      if (!ill && lg == 0) flags |= other ? azb::kFlagNoPlace : (azb::kFlagNoPlace | azb::kFlagTerminal);
+      oo[i] = no; po[i] = np; lo[i] = lg;
+      so[i] = ill ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(flags, azb::popc(no) - azb::popc(np));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void v12(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS {
+    uint64_t no, np; int flags; bool ill;
+    y::step_core(own[i], opp[i], act[i], no, np, flags, ill);
+    oo[i] = no; po[i] = np; lo[i] = no | np; so[i] = azb::pack_status(flags, azb::popc(no) - azb::popc(np));
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9};
-  if (v < 0 || v > 9) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12};
+  if (v < 0 || v > 12) return -1;
   hipLaunchKernelGGL(ks[v], dim3(grid), dim3(256), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
