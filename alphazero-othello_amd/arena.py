@@ -1,0 +1,166 @@
+"""Batched arena evaluation on the GPU engine: eval.py's play_match / evaluate_models
+(eval.py:12-44, 46-74, 134-178) for many matches at once.
+
+Each net owns one host-driven engine whose slot g is that net's tree in match g (the
+reference gives each player its own `MCTS` with tree reuse).  Per ply, every match's side
+to move searches in its own engine (temperature 0, no root noise: eval.py builds its
+trees with the default dirichlet_epsilon = 0); both engines' searches run concurrently,
+one leaf per searching slot per step; the action is the argmax of the root visit counts
+with the reference's random tie break (np.random.choice over the tied maxima,
+MCTS_model.py:250-254); the board advances through the C-ABI step; both trees re-root on
+the action (eval.py:176-177).  Colours alternate by match index as in
+evaluate_models_parallel (even: A plays first).
+"""
+import numpy as np
+import torch
+
+import az_native as nat
+from engine import Engine
+
+INIT_OWN, INIT_OPP = 0x0000000810000000, 0x0000001008000000
+
+
+def _as_evaluator(net, device):
+    """nn.Module -> batched device evaluator over the engine's planes; callables pass
+    through (device-side test policies); None = rollout evaluation."""
+    if net is None or callable(net) and not isinstance(net, torch.nn.Module):
+        return net
+    from Models import inference_copy
+
+    m = inference_copy(net, device)
+    return m.evaluate_planes
+
+
+def tie_break_random(best):
+    return int(np.random.choice(best))
+
+
+def tie_break_lowest(best):
+    return int(best[0])
+
+
+class BatchedArena:
+    def __init__(self, net_a, net_b, args, n_slots, device=None, seed=0,
+                 tie_break=tie_break_random, node_capacity=0):
+        self.args = args
+        self.G = n_slots
+        kw = dict(c_puct=args["c_puct"], auto_play=False, node_capacity=node_capacity,
+                  device=device)
+        self.eng = [Engine(n_slots, args["num_simulations"], rollout=net_a is None, seed=seed,
+                           **kw),
+                    Engine(n_slots, args["num_simulations"], rollout=net_b is None,
+                           seed=seed + 1, **kw)]
+        dev = self.eng[0].device
+        self.eval = [_as_evaluator(net_a, dev), _as_evaluator(net_b, dev)]
+        self.tie_break = tie_break
+
+    def _search(self, slots, check_every=8):
+        sims = self.args["num_simulations"]
+        live = []
+        for k in (0, 1):
+            if len(slots[k]):
+                self.eng[k].begin_search_slots(slots[k], sims)
+                live.append(k)
+        with torch.no_grad():
+            while live:
+                for _ in range(check_every):
+                    for k in live:
+                        e = self.eng[k]
+                        e.select()
+                        if self.eval[k] is not None:
+                            pr, va = self.eval[k](e.nn_in)
+                            e.priors.copy_(pr)
+                            e.values.copy_(va)
+                        e.expand()
+                live = [k for k in live
+                        if (self.eng[k].game_info()["status"] == nat.AZ_GAME_ACTIVE).any()]
+
+    def play(self, n_matches):
+        """Play n_matches (in waves of G) and return (wins_a, wins_b, draws, plies)."""
+        wins_a = wins_b = draws = 0
+        plies = []
+        for base in range(0, n_matches, self.G):
+            n = min(self.G, n_matches - base)
+            a_first = (np.arange(base, base + n) % 2) == 0
+            res, pl = self._play_wave(a_first)
+            wins_a += int((res == 1).sum())
+            wins_b += int((res == -1).sum())
+            draws += int((res == 0).sum())
+            plies.extend(pl)
+        return wins_a, wins_b, draws, plies
+
+    def _play_wave(self, a_first):
+        n = len(a_first)
+        own = np.full(n, INIT_OWN, np.uint64)
+        opp = np.full(n, INIT_OPP, np.uint64)
+        player = np.ones(n, np.int32)
+        live = np.ones(n, bool)
+        has_root = np.zeros((2, n), bool)
+        result = np.zeros(n, np.int32)  # +1 A won, -1 B won, 0 draw
+        ply = np.zeros(n, np.int32)
+        while live.any():
+            # engine of the side to move: 0 (A) when A plays this colour
+            mover = np.where((player == 1) == a_first, 0, 1)
+            slots = []
+            for k in (0, 1):
+                sel = np.nonzero(live & (mover == k))[0]
+                fresh = sel[~has_root[k][sel]]
+                if len(fresh):  # policy_improve_step with root None (MCTS_model.py:223-228)
+                    self.eng[k].set_roots(fresh, own[fresh], opp[fresh], player[fresh])
+                    has_root[k][fresh] = True
+                slots.append(sel.astype(np.int32))
+            self._search(slots)
+            actions = np.full(n, -1, np.int64)
+            for k in (0, 1):
+                if not len(slots[k]):
+                    continue
+                counts, _ = self.eng[k].root_stats()
+                for g in slots[k]:
+                    c = counts[g].astype(np.float32)
+                    best = np.where(c == c.max())[0]
+                    actions[g] = self.tie_break(best)
+            idx = np.nonzero(live)[0]
+            o, p, _, st = nat.step_cpu(own[idx], opp[idx], actions[idx].astype(np.uint8))
+            terminal = (nat.status_flags(st) & nat.AZ_FLAG_TERMINAL) != 0
+            score = nat.status_score(st)  # side to move after the step minus the mover
+            for j, g in enumerate(idx):
+                ply[g] += 1
+                if terminal[j]:
+                    # reward from the mover's view (eval.py:163-175)
+                    d = -score[j]
+                    winner_is_a = (mover[g] == 0) if d > 0 else (mover[g] == 1)
+                    result[g] = 0 if d == 0 else (1 if winner_is_a else -1)
+                    live[g] = False
+            own[idx], opp[idx] = o, p
+            player[idx] = -player[idx]
+            # both trees re-root on the action (eval.py:176-177); no-op without a root
+            for k in (0, 1):
+                act = np.full(self.G, -1, np.int32)
+                sel = np.nonzero(live & has_root[k])[0]
+                act[sel] = actions[sel]
+                if len(sel):
+                    found = self.eng[k].reroot_slots(act)
+                    missing = sel[found[sel] < 0]
+                    if len(missing):
+                        raise KeyError(int(actions[missing[0]]))
+        return result, list(ply)
+
+
+def evaluate_models_batched(board_size, args, policy_state, best_policy_state, n_matches=20,
+                            n_slots=None, device=None):
+    """Drop-in for evaluate_models_parallel (eval.py:46-74): returns
+    (win rate of `policy`, win rate of `best_policy`)."""
+    assert board_size == 8
+
+    def build(ps):
+        if ps is None:
+            return None
+        cls, cfg, sd = ps
+        net = cls(**cfg)
+        net.load_state_dict(sd)
+        return net.eval()
+
+    arena = BatchedArena(build(policy_state), build(best_policy_state), args,
+                         n_slots or min(n_matches, 1024), device=device)
+    wa, wb, _, _ = arena.play(n_matches)
+    return wa / n_matches, wb / n_matches

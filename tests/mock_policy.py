@@ -18,9 +18,19 @@ A = ((_i * 131 + _j * 71 + _i * _j * 7) % 97).astype(np.int64)  # [65, 64]
 B = ((np.arange(64, dtype=np.int64) * 37 + 11) % 89).astype(np.int64)  # [64]
 
 
-def mock_eval(canonical):
+def _mats(salt):
+    """salt 0 = the golden-vector policy; other salts = distinct "nets" (arena tests)."""
+    if salt == 0:
+        return A, B
+    a = ((_i * 131 + _j * 71 + _i * _j * 7 + 13 * salt) % 97).astype(np.int64)
+    b = ((np.arange(64, dtype=np.int64) * 37 + 11 + 5 * salt) % 89).astype(np.int64)
+    return a, b
+
+
+def mock_eval(canonical, salt=0):
     """canonical: int array [..., 64] with values in {-1, 0, +1}.
     Returns priors float32 [..., 65] and values float64 [...] (float32-exact)."""
+    A, B = _mats(salt)
     x = np.asarray(canonical).astype(np.int64) + 1
     h = (x @ A.T) % 1021 + 1
     priors = h.astype(np.float32) / np.float32(1024)
@@ -61,12 +71,13 @@ def mock_eval_planes(nn_in):
     return p, v.astype(np.float32)
 
 
-def mock_eval_torch(planes):
+def mock_eval_torch(planes, salt=0):
     """The same closed form on device (torch float64 matmuls are exact here: every partial
     sum is an integer below 2^53).  planes: float32 [G, 64] -> (priors f32 [G, 65],
     values f32 [G])."""
     import torch
 
+    A, B = _mats(salt)
     x = torch.round(planes.double()) + 1.0
     At = torch.as_tensor(A.T, dtype=torch.float64, device=planes.device)
     Bt = torch.as_tensor(B, dtype=torch.float64, device=planes.device)
