@@ -109,6 +109,12 @@ SIGNATURES = {
 
 
 def _load():
+    # torch ships its own HIP runtime and preloads it by path; loading ours first would put
+    # a second copy of libamdhip64 / libhsa-runtime64 in the process (the second HSA
+    # instance then sees no device).  With torch loaded first, the library's
+    # libamdhip64.so.7 dependency resolves to torch's copy by soname: one runtime.
+    import torch  # noqa: F401
+
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` (build()) "

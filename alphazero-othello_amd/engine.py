@@ -253,7 +253,7 @@ class BatchedSelfPlay:
 
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
-                 device=None, fold=True):
+                 device=None, fold=True, steps_per_graph=8):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -274,7 +274,8 @@ class BatchedSelfPlay:
         else:
             self.net = net.to(self.device).eval()
         self.use_graph = use_graph
-        self.graph = None
+        self.steps_per_graph = max(1, int(steps_per_graph))
+        self.graph = None  # {steps: CUDAGraph}: one replay = that many simulation steps
 
     def _step_body(self):
         e = self.engine
@@ -287,16 +288,24 @@ class BatchedSelfPlay:
         e.play()
 
     def _capture(self):
+        """Capture the step into HIP graphs: one of `steps_per_graph` consecutive steps (the
+        host launches one graph per that many steps, so launch cost never paces the GPU)
+        and one single step for remainders.  The steps are pure device work on engine state
+        in HBM, so replaying a captured sequence is the same computation."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm MIOpen / hipBLASLt solution caches outside capture
                 self._step_body()
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g):
-            self._step_body()
-        self.graph = g
+        graphs = {}
+        for k in sorted({1, self.steps_per_graph}):
+            g = torch.cuda.CUDAGraph()  # private memory pool per graph
+            with torch.no_grad(), torch.cuda.graph(g):
+                for _ in range(k):
+                    self._step_body()
+            graphs[k] = g
+        self.graph = graphs
 
     def reset(self, start_budget=-1, stagger_steps=0):
         self.engine.reset_all(start_budget, stagger_steps)
@@ -309,11 +318,15 @@ class BatchedSelfPlay:
             except Exception as ex:  # capture unsupported for this net: run eagerly
                 self.use_graph = False
                 self.graph_error = repr(ex)
-        for _ in range(n):
-            if self.graph is not None:
-                self.graph.replay()
-            else:
+        if self.graph is None:
+            for _ in range(n):
                 self._step_body()
+            return
+        k = self.steps_per_graph
+        for _ in range(n // k):
+            self.graph[k].replay()
+        for _ in range(n % k):
+            self.graph[1].replay()
 
     def play_games(self, n_games, max_steps=None, check_every=256):
         """Play exactly n_games complete games (slots restart until the budget is used);

@@ -54,7 +54,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8000)
-    ap.add_argument("--warmup", type=int, default=4000)
+    ap.add_argument("--warmup", type=int, default=24000,
+                    help="untimed steps; the default (about one game length at 400 sims) lets "
+                         "the first games finish so plies/game is measured in this run")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
                     help="BASELINE.json configs: c2 = 4096 games x 100 sims FastOthelloNet; "
                          "c3 = 1024 games x 400 sims AlphaZeroNet(5x128) fp32 (the metric's "
@@ -207,7 +209,7 @@ def main():
     e = sp.engine
     # stagger slot starts over the warmup (at least one move length) so moves complete at a
     # steady rate in the window
-    sp.reset(start_budget=-1, stagger_steps=max(1, a.warmup))
+    sp.reset(start_budget=-1, stagger_steps=max(1, min(a.warmup, (a.sims + 1) * 20)))
 
     def barrier():
         torch.cuda.synchronize()

@@ -19,7 +19,10 @@ def pytest_configure(config):
 
 
 def load_golden(name):
-    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    """Fixture arrays as a plain dict (an NpzFile would re-read and decompress the member on
+    every d[key] access)."""
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
 
 
 @pytest.fixture(scope="session")
