@@ -1268,7 +1268,11 @@ int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
   AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select: null argument");
   hipStream_t s = azc::as_stream(stream);
   AZ_HIP(hipMemsetAsync(&e->p.ctr->ready_n, 0, sizeof(int32_t), s));
-  const int max_descents = 4 * (e->p.sims + 1) + 64;
+  // Simulations that end on a terminal node need no evaluation and run inside the select
+  // call; cap them per step so one end-game tree (every simulation terminal) cannot hold
+  // the whole batched step for hundreds of dependent descents.  Host-driven engines step
+  // one search at a time and take them all at once.
+  const int max_descents = e->p.auto_play ? 4 : 4 * (e->p.sims + 1) + 64;
   hipLaunchKernelGGL(k_select, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in, leaf_o,
                      max_descents);
   AZ_HIP(hipGetLastError());

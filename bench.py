@@ -131,6 +131,39 @@ def kernel_roofline(positions, n, device):
     return ms, n
 
 
+def conv_roofline(sp, device, n_boards):
+    """The step's dominant kernel (k_conv3x3: ~90 % of a step's GPU time) timed with HIP
+    events on its launch stream, at the bench's leaf batch, with the net's own weights:
+    achieved = 2*B*64*C*C*9 FLOP per launch / average launch time, against the dense fp32
+    MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md)."""
+    import az_native as nat
+
+    conv = sp.net.c2[0]
+    C = conv.channels
+    x = torch.randn(n_boards, C, 8, 8, device=device).contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    y = torch.empty_like(x)
+    args = [nat.ptr(x), nat.ptr(conv.w9), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y), n_boards, C,
+            1, nat.stream_ptr()]
+    for _ in range(3):
+        nat.check(nat.lib.az_conv3x3_gpu(*args), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    ev0.record()
+    for _ in range(reps):
+        nat.lib.az_conv3x3_gpu(*args)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / reps
+    flop = 2.0 * n_boards * 64 * C * C * 9
+    achieved = flop / (ms * 1e-3) / 1e12
+    return {"kernel": "k_conv3x3 (az_conv3x3_gpu, fused bias+residual+ReLU)", "bound": "mfma",
+            "achieved": round(achieved, 1), "peak": 157.3, "unit": "TFLOP/s",
+            "frac": round(achieved / 157.3, 4), "traffic": None, "boards": n_boards,
+            "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop}
+
+
 def cpu_baseline(net, seconds):
     """The oracle's restatement of one_self_play (reference algorithm, sequential MCTS,
     batch-1 torch-CPU inference, C board oracle), timed for a bounded sample of moves of one
@@ -304,6 +337,9 @@ def main():
                               "traffic": traffic, "positions": n,
                               "avg_launch_ms": round(ms, 4),
                               "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
+    if rank == 0 and world == 1 and not a.skip_kernel and hasattr(sp.net, "c2") \
+            and getattr(sp.net, "conv_impl", "") == "hip":
+        result["roofline_conv"] = conv_roofline(sp, device, a.games)
     if rank == 0 and world == 1 and not a.skip_cpu:
         result["cpu_baseline"] = cpu_baseline(make_net(a.net), a.cpu_seconds)
         result["cpu_baseline"]["cores"] = 1

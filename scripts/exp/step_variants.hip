@@ -238,11 +238,50 @@ __global__ __launch_bounds__(256) void v12(const uint64_t* own, const uint64_t* 
   }
 }
 
+// v13: product step, two positions per lane (16-byte own/opp/legal I/O)
+__global__ __launch_bounds__(256) void v13(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t n2 = n / 2;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n2; j += (int64_t)gridDim.x * 256) {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2*>(own)[j];
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(opp)[j];
+    const uint16_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    azb::Step s0 = azb::step(a.x, b.x, c & 0xFF), s1 = azb::step(a.y, b.y, c >> 8);
+    reinterpret_cast<ulonglong2*>(oo)[j] = make_ulonglong2(s0.own, s1.own);
+    reinterpret_cast<ulonglong2*>(po)[j] = make_ulonglong2(s0.opp, s1.opp);
+    reinterpret_cast<ulonglong2*>(lo)[j] = make_ulonglong2(s0.legal, s1.legal);
+    reinterpret_cast<uint32_t*>(so)[j] = (uint32_t)s0.status | ((uint32_t)s1.status << 16);
+  }
+}
+// v14: product step, block 64 / v15: block 512 (same body as v0)
+__global__ __launch_bounds__(64) void v14(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 64) {
+    azb::Step s = azb::step(own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+}
+// v16: four positions per lane, loads for all four issued before any compute
+__global__ __launch_bounds__(256) void v16(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t q = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < q; j += stride) {
+    uint64_t a[4], b[4]; int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const int64_t i = j + k * q; a[k] = own[i]; b[k] = opp[i]; c[k] = act[i]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = j + k * q;
+      azb::Step s = azb::step(a[k], b[k], c[k]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    }
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12};
-  if (v < 0 || v > 12) return -1;
-  hipLaunchKernelGGL(ks[v], dim3(grid), dim3(256), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16};
+  if (v < 0 || v > 16) return -1;
+  const int blk = v == 14 ? 64 : 256;
+  hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
