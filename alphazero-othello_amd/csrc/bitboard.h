@@ -132,33 +132,103 @@ AZ_HD int terminal_flags(uint64_t own, uint64_t opp, uint64_t lg) {
   return legal(opp, own) ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
 }
 
+// ---- wave-cooperative terminal check (device) ----------------------------------------
+// Legal placements of P against O along ONE direction d (0..3: shifts towards higher bits
+// by 1, 8, 7, 9; 4..7: the same towards lower bits), the fill of legal() split by direction
+// so that eight lanes can share one position.
+__device__ __forceinline__ uint64_t dir_moves(uint64_t P, uint64_t O, int d) {
+  const int s = (0x09070801 >> ((d & 3) * 8)) & 0xFF;
+  const uint64_t M = (d & 3) == 1 ? O : (O & kInner);
+  const bool up = d < 4;
+  uint64_t x = M & (up ? (P << s) : (P >> s));
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x |= M & (up ? (x << s) : (x >> s));
+  return (up ? (x << s) : (x >> s)) & ~(P | O);
+}
+
+// terminal_flags() for one position per lane, computed by the whole wavefront: the rare
+// lanes that need the opponent's full fill (no placement, no cheap proof) are served eight
+// lanes per position — one direction each — up to eight positions per pass, instead of the
+// whole wavefront executing a divergent full legal() for them.  Every lane of the wave must
+// call it (uniform control flow); `live` marks lanes that hold a position.
+__device__ __forceinline__ int terminal_flags_wave(uint64_t own, uint64_t opp, uint64_t lg,
+                                                   bool live) {
+  if (!live || lg) return 0;
+  if ((own | opp) == ~0ull || own == 0 || opp == 0) return kFlagNoPlace | kFlagTerminal;
+  return -1;  // needs the cooperative pass
+}
+
+__device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp) {
+  const int lane = __lane_id();
+  uint64_t need = __ballot(flags < 0);
+  bool other = false;
+  while (need) {
+    const int grp = lane >> 3;
+    uint64_t m = need;
+    for (int j = 0; j < grp && m; ++j) m &= m - 1;
+    const int src = m ? __builtin_ctzll(m) : lane;
+    const uint64_t P = __shfl(opp, src, 64), O = __shfl(own, src, 64);
+    const uint64_t mv = m ? dir_moves(P, O, lane & 7) : 0ull;
+    const uint64_t any = __ballot(mv != 0);
+    if ((need >> lane) & 1) {
+      const int rank = popc(need & ((1ull << lane) - 1ull));
+      if (rank < 8) other = ((any >> (8 * rank)) & 0xFFull) != 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) need &= need - 1;
+  }
+  if (flags >= 0) return flags;
+  return other ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
+}
+
+struct Move {
+  uint64_t own, opp;  // next side to move, its opponent (inputs unchanged when illegal)
+  int flags;          // kFlagPassed for the pass
+  bool illegal;
+};
+
+// The make-move half of step(): placement with flips (or pass), illegal placements
+// detected (no capture, occupied square or out of range) and left unchanged.
+AZ_HD Move move(uint64_t own, uint64_t opp, int act) {
+  Move m;
+  m.flags = 0;
+  m.illegal = false;
+  if (act == kPass) {
+    m.own = opp;
+    m.opp = own;
+    m.flags = kFlagPassed;
+    return m;
+  }
+  const bool in_range = (unsigned)act < 64u;
+  const int sq = act & 63;
+  const uint64_t nb = 1ull << sq;
+  const uint64_t cap = in_range ? flips(own, opp, sq) : 0ull;
+  if (!in_range || cap == 0ull || (nb & (own | opp))) {
+    m.own = own;
+    m.opp = opp;
+    m.illegal = true;
+    return m;
+  }
+  m.own = opp ^ cap;
+  m.opp = (own | nb) ^ cap;
+  return m;
+}
+
 // One board step for one position: placement or pass, then the next side's legal mask,
 // terminal check and disc difference.  Illegal placements leave the board unchanged and
 // set kFlagIllegal (the reference raises ValueError at envs/othello.py:419-421).
 AZ_HD Step step(uint64_t own, uint64_t opp, int act) {
   Step o;
-  int flags = 0;
-  if (act == kPass) {
-    o.own = opp;
-    o.opp = own;
-    flags = kFlagPassed;
-  } else {
-    const bool in_range = (unsigned)act < 64u;
-    const int sq = act & 63;
-    const uint64_t nb = 1ull << sq;
-    const uint64_t cap = in_range ? flips(own, opp, sq) : 0ull;
-    if (!in_range || cap == 0ull || (nb & (own | opp))) {
-      o.own = own;
-      o.opp = opp;
-      o.legal = 0;
-      o.status = pack_status(kFlagIllegal, 0);
-      return o;
-    }
-    o.own = opp ^ cap;
-    o.opp = (own | nb) ^ cap;
+  const Move m = move(own, opp, act);
+  o.own = m.own;
+  o.opp = m.opp;
+  if (m.illegal) {
+    o.legal = 0;
+    o.status = pack_status(kFlagIllegal, 0);
+    return o;
   }
   o.legal = legal(o.own, o.opp);
-  flags |= terminal_flags(o.own, o.opp, o.legal);
+  const int flags = m.flags | terminal_flags(o.own, o.opp, o.legal);
   o.status = pack_status(flags, popc(o.own) - popc(o.opp));
   return o;
 }

@@ -44,13 +44,31 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
                                                  uint64_t* __restrict__ legal_o,
                                                  uint16_t* __restrict__ status_o,
                                                  int64_t n) {
+  // every lane runs the same number of iterations (the terminal check is wave-cooperative)
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    const azb::Step s = azb::step(own[i], opp[i], act[i]);
-    own_o[i] = s.own;
-    opp_o[i] = s.opp;
-    legal_o[i] = s.legal;
-    status_o[i] = s.status;
+  const int64_t n_pad = (n + kBlock - 1) / kBlock * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    uint64_t o = 0, p = 0;
+    int a = azb::kPass;
+    if (live) {
+      o = own[i];
+      p = opp[i];
+      a = act[i];
+    }
+    const azb::Move mv = azb::move(o, p, a);
+    const bool ok = live && !mv.illegal;
+    const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+    int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+    tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+    if (live) {
+      own_o[i] = mv.own;
+      opp_o[i] = mv.opp;
+      legal_o[i] = lg;
+      status_o[i] = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0)
+                               : azb::pack_status(mv.flags | tf,
+                                                  azb::popc(mv.own) - azb::popc(mv.opp));
+    }
   }
 }
 

@@ -457,13 +457,18 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
   fc = shfl(fc, 0);
   if (fc >= 0) {
     const bool mine = lg ? valid : (lane == 0);
+    const int a = lg ? lane : azb::kPass;
+    uint64_t co = 0, cp = 0, clg = 0;
     if (mine) {
-      const int a = lg ? lane : azb::kPass;
-      const int ci = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
-      uint64_t co, cp;
       azb::play(own, opp, a, lg ? azb::flips(own, opp, a) : 0ull, &co, &cp);
-      const uint64_t clg = azb::legal(co, cp);
-      const bool term = (azb::terminal_flags(co, cp, clg) & azb::kFlagTerminal) != 0;
+      clg = azb::legal(co, cp);
+    }
+    // terminal check of every child, wave-cooperative for the rare real passes
+    int tf = azb::terminal_flags_wave(co, cp, clg, mine);
+    tf = azb::finish_terminal_wave(tf, co, cp);
+    if (mine) {
+      const int ci = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
+      const bool term = (tf & azb::kFlagTerminal) != 0;
       const int d = azb::popc(co) - azb::popc(cp);
       const int64_t c = nidx(p, half, g, fc + ci);
       p.a.own[c] = co;
