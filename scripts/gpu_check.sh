@@ -21,4 +21,11 @@ STEPS=${STEPS:-all}
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench 900 python bench.py ${BENCH_ARGS:-}
 [[ $STEPS == *prof* || $STEPS == all ]] && run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --skip-cpu ${PROF_ARGS:---steps 400 --warmup 200}
+[[ $STEPS == *skb* ]] && run skb 120 python scripts/step_kernel_bench.py
+[[ $STEPS == *nnmb* ]] && run nnmb 300 python scripts/nn_microbench.py 1024
+[[ $STEPS == *convb* ]] && run convb 300 python scripts/conv_bench.py
+[[ $STEPS == *variants* ]] && run variants 300 python scripts/exp/run_step_variants.py
+[[ $STEPS == *breakdown* ]] && run breakdown 600 python scripts/step_breakdown.py ${BREAKDOWN_STEPS:-30000}
+[[ $STEPS == *pmc* ]] && run pmc 900 bash scripts/pmc_step.sh
+[[ $STEPS == *rehearse* ]] && run rehearse 600 env AZ_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 400 --warmup 200 --skip-cpu --skip-kernel
 exit 0
