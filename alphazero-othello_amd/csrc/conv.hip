@@ -48,9 +48,10 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
   const int b0 = blockIdx.x * kBoards;
   const int nb = n_boards - b0 < kBoards ? n_boards - b0 : kBoards;
 
-  // ---- stage the input boards (NHWC) into LDS, zero-fill a missing tail board
+  // ---- stage the input boards (NHWC) into LDS, zero-fill a missing tail board; one extra
+  // all-zero position (index kBoards*64) is what off-board taps read (branch-free gather)
   {
-    constexpr int V = kBoards * 64 * C / 4;  // float4s
+    constexpr int V = (kBoards * 64 + 1) * C / 4;  // float4s
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
     for (int v = tid; v < V; v += kThreads) {
       const int pos = v / (C / 4), c4 = v % (C / 4);
@@ -97,6 +98,7 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
     for (int ni = 0; ni < G::TN; ++ni)
       b[ni] = *reinterpret_cast<const float4*>(wcol[ni] + (size_t)tap * C * C + ci0);
   };
+  constexpr int kZeroPos = kBoards * 64;
   auto load_a = [&](int s, float4 (&a)[G::TM]) {
     const int tap = s / CHUNKS, ci0 = (s % CHUNKS) * 8;
     const int ky = tap / 3 - 1, kx = tap % 3 - 1;
@@ -104,36 +106,44 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
     for (int mi = 0; mi < G::TM; ++mi) {
       const int yy = py[mi] + ky, xx = px[mi] + kx;
       const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
-      const int pos = pb[mi] * 64 + (ok ? yy * 8 + xx : 0);
-      const float4 v = *reinterpret_cast<const float4*>(lds + pos * G::S + ci0 + 4 * h);
-      a[mi] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int pos = ok ? pb[mi] * 64 + yy * 8 + xx : kZeroPos;
+      a[mi] = *reinterpret_cast<const float4*>(lds + pos * G::S + ci0 + 4 * h);
     }
   };
-
-  float4 a_cur[G::TM], b_cur[G::TN], a_nxt[G::TM], b_nxt[G::TN];
-  load_b(0, b_cur);
-  load_a(0, a_cur);
-  for (int s = 0; s < STEPS; ++s) {
-    if (s + 1 < STEPS) {
-      load_b(s + 1, b_nxt);
-      load_a(s + 1, a_nxt);
-    }
+  auto mma = [&](const float4 (&a)[G::TM], const float4 (&b)[G::TN]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int mi = 0; mi < G::TM; ++mi) {
-        const float av = j == 0 ? a_cur[mi].x : j == 1 ? a_cur[mi].y : j == 2 ? a_cur[mi].z : a_cur[mi].w;
+        const float av = j == 0 ? a[mi].x : j == 1 ? a[mi].y : j == 2 ? a[mi].z : a[mi].w;
 #pragma unroll
         for (int ni = 0; ni < G::TN; ++ni) {
-          const float bv = j == 0 ? b_cur[ni].x : j == 1 ? b_cur[ni].y : j == 2 ? b_cur[ni].z : b_cur[ni].w;
+          const float bv = j == 0 ? b[ni].x : j == 1 ? b[ni].y : j == 2 ? b[ni].z : b[ni].w;
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[mi][ni], 0, 0, 0);
         }
       }
     }
-#pragma unroll
-    for (int mi = 0; mi < G::TM; ++mi) a_cur[mi] = a_nxt[mi];
-#pragma unroll
-    for (int ni = 0; ni < G::TN; ++ni) b_cur[ni] = b_nxt[ni];
+  };
+
+  // two chunks in flight: ping-pong register sets, loads for chunk s+2 issued right after
+  // chunk s's MFMAs (no register copies, no full drain per chunk)
+  static_assert(STEPS % 2 == 0, "even number of (tap, chunk) steps");
+  float4 ra0[G::TM], rb0[G::TN], ra1[G::TM], rb1[G::TN];
+  load_b(0, rb0);
+  load_a(0, ra0);
+  load_b(1, rb1);
+  load_a(1, ra1);
+  // the prefetches are unconditional (clamped to the last chunk) so the compiler's
+  // vmcnt/lgkmcnt bookkeeping stays exact: each MFMA group waits only for its own chunk
+  for (int s = 0; s < STEPS; s += 2) {
+    mma(ra0, rb0);
+    const int s2 = s + 2 < STEPS ? s + 2 : STEPS - 2;
+    load_b(s2, rb0);
+    load_a(s2, ra0);
+    mma(ra1, rb1);
+    const int s3 = s + 3 < STEPS ? s + 3 : STEPS - 1;
+    load_b(s3, rb1);
+    load_a(s3, ra1);
   }
 
   // ---- epilogue: D[row][col], col = lane&31, row = (k&3) + 8*(k>>2) + 4*(lane>>5)
@@ -196,7 +206,7 @@ template <class G>
 int launch_conv(const float* x, const float* w, const float* bias, const float* res, float* y,
                 int n_boards, int relu, hipStream_t s) {
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
-  const size_t lds = (size_t)G::BOARDS * 64 * G::S * sizeof(float);
+  const size_t lds = (size_t)(G::BOARDS * 64 + 1) * G::S * sizeof(float);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in once per kernel
   if (!attr_set) {
     const void* ks[] = {(const void*)k_conv3x3<G, true, true>, (const void*)k_conv3x3<G, true, false>,

@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--net", default=None, choices=["az5x128", "fast"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=8,
+                    help="simulation steps captured per HIP graph (1 under rocprofv3: its "
+                         "kernel tracer crashes on multi-step captures)")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--skip-cpu", action="store_true")
@@ -238,7 +241,7 @@ def main():
     sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
                          use_graph=not a.no_graph, device=device, d4_augment=a.d4,
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
-                         sample_capacity=a.games * 130 * 4)
+                         sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph)
     e = sp.engine
     # stagger slot starts over the warmup (at least one move length) so moves complete at a
     # steady rate in the window

@@ -22,9 +22,19 @@ def main():
     ap.add_argument("--steps", type=int, default=0)
     ap.add_argument("--top", type=int, default=25)
     a = ap.parse_args()
-    c = sqlite3.connect(a.db)
-    rows = list(c.execute("select name, total_calls, total_duration, average, percentage "
-                          "from top_kernels order by total_duration desc"))
+    if a.db.endswith(".csv"):
+        # rocprofv3 --stats --output-format csv: <run>_kernel_stats.csv (durations in ns)
+        import csv
+
+        rows = []
+        for r in csv.DictReader(open(a.db)):
+            rows.append((r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3,
+                         float(r["AverageNs"]) / 1e3, float(r["Percentage"])))
+        rows.sort(key=lambda r: -r[2])
+    else:
+        c = sqlite3.connect(a.db)
+        rows = list(c.execute("select name, total_calls, total_duration, average, percentage "
+                              "from top_kernels order by total_duration desc"))
     tot = sum(r[2] for r in rows)
     print(f"source: `{a.db}` (rocprofv3 --kernel-trace --stats); durations in microseconds\n")
     hdr = "| kernel | calls | total us | avg us | % |"
