@@ -229,16 +229,17 @@ int launch_conv(const float* x, const float* w, const float* bias, const float* 
 }
 
 // tiling candidates (C, boards, waves, TM, TN); index 0 of each C is the default, picked
-// by scripts/conv_bench.py on MI355X (B = 1024: C=128 176 us vs MIOpen's 175 us for the
-// bare convolution; C=64 51 us vs 59 us)
-using G128_0 = Geo<128, 2, 8, 1, 2>;
-using G128_1 = Geo<128, 1, 4, 1, 2>;
+// by scripts/conv_bench.py on MI355X with the pipelined main loop (B = 1024, one run:
+// C=128 164 us = 118 TFLOP/s vs MIOpen's 191 us for the bare convolution; C=64 49 us vs 57)
+using G128_0 = Geo<128, 2, 4, 2, 2>;
+using G128_1 = Geo<128, 1, 2, 2, 2>;
 using G128_2 = Geo<128, 4, 8, 2, 2>;
-using G128_3 = Geo<128, 2, 4, 2, 2>;
-using G128_4 = Geo<128, 1, 2, 2, 2>;
-using G64_0 = Geo<64, 1, 2, 1, 2>;
-using G64_1 = Geo<64, 2, 4, 1, 2>;
-using G64_2 = Geo<64, 4, 4, 2, 2>;
+using G128_3 = Geo<128, 2, 2, 4, 2>;
+using G128_4 = Geo<128, 4, 4, 4, 2>;
+using G128_5 = Geo<128, 2, 8, 1, 2>;
+using G64_0 = Geo<64, 4, 4, 2, 2>;
+using G64_1 = Geo<64, 1, 2, 1, 2>;
+using G64_2 = Geo<64, 4, 2, 4, 2>;
 
 int launch_cfg(int cfg, const float* x, const float* w, const float* bias, const float* res,
                float* y, int n_boards, int channels, int relu, hipStream_t s) {
@@ -249,6 +250,7 @@ int launch_cfg(int cfg, const float* x, const float* w, const float* bias, const
       case 2: return launch_conv<G128_2>(x, w, bias, res, y, n_boards, relu, s);
       case 3: return launch_conv<G128_3>(x, w, bias, res, y, n_boards, relu, s);
       case 4: return launch_conv<G128_4>(x, w, bias, res, y, n_boards, relu, s);
+      case 5: return launch_conv<G128_5>(x, w, bias, res, y, n_boards, relu, s);
     }
   } else if (channels == 64) {
     switch (cfg) {

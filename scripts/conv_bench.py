@@ -7,7 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "alphazero-othello_amd"))
 import az_native as nat  # noqa: E402
 
-CFGS = {128: [0, 1, 2, 3, 4], 64: [0, 1, 2]}
+CFGS = {128: [0, 1, 2, 3, 4, 5], 64: [0, 1, 2]}
 
 
 def timed(fn, reps=30):
