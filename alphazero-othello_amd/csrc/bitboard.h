@@ -13,10 +13,15 @@
 // compute the same rule-defined sets with fewer integer ops (the rule-defined legal set
 // and capture set are unique, so equality with the reference is a property of the rules;
 // tests/ check it against the oracle and the reference-generated golden vectors):
-//   * legal():  direction-pair occluded fill with propagator doubling (3 fill steps per
-//               direction instead of 6);
+//   * legal():  horizontal moves by carry propagation (the downward direction on the
+//               bit-reversed board), the other three direction pairs by occluded fill with
+//               propagator doubling (3 fill steps per direction instead of 6), every
+//               three-input and/or step one v_bitop3_b32 per half on gfx950;
 //   * flips():  per-line ray masks built arithmetically, first non-opponent square found
-//               with a bit-scan (lowest bit upward, highest bit downward).
+//               with a bit-scan (lowest bit upward, highest bit downward);
+//   * flips_rays(): the batched kernels' form — the eight rays of the placed square from
+//               a 2 KB up-ray table (down-rays = up-rays of 63 - sq on the bit-reversed
+//               board), each ray's capture found with one subtraction (o - 1).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -44,30 +49,137 @@ enum : int {
 
 AZ_HD int popc(uint64_t x) { return __builtin_popcountll(x); }
 
-// Candidate moves of P through masked opponent stones M along +D and -D.
+// ---- three-input bitwise ops ---------------------------------------------------------
+// bop3<T>(a, b, c): any boolean function of three words in one v_bitop3_b32 per 32-bit
+// half on gfx950 (the compiler does not form it from 64-bit and/or chains).  T is the
+// truth table over a = 0xF0, b = 0xCC, c = 0xAA, e.g. T(a | (b & c)) = 0xF8.
+namespace tt {
+constexpr uint8_t A = 0xF0, B = 0xCC, C = 0xAA;
+}
+template <uint8_t T>
+AZ_HD uint64_t bop3(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, T);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32),
+                                                  (uint32_t)(c >> 32), T);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  uint64_t r = 0;
+  for (int i = 0; i < 8; ++i)
+    if ((T >> i) & 1) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+  return r;
+#endif
+}
+// 180-degree rotation of the board = bit reversal of the word (v_bfrev_b32 x 2): square
+// r*8+c -> (7-r)*8+(7-c), so a ray towards lower bit indices becomes one towards higher.
+AZ_HD uint64_t rev64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) |
+         __builtin_bitreverse32((uint32_t)(x >> 32));
+#else
+  return __builtin_bitreverse64(x);
+#endif
+}
+
+// Whole-word shifts by a constant.  On the device they are pinned to one v_lshlrev_b64 /
+// v_lshrrev_b64 on a register pair: left to itself the compiler narrows a 64-bit shift
+// whose halves feed bop3 into two or three 32-bit ops.
+template <int S>
+AZ_HD uint64_t shl(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r;
+  asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+  return r;
+#else
+  return x << S;
+#endif
+}
+template <int S>
+AZ_HD uint64_t shr(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r;
+  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+  return r;
+#else
+  return x >> S;
+#endif
+}
+
+// Candidate moves of P through masked opponent stones M along +D and -D: occluded fill
+// with propagator doubling (1 + 1 + 2 + 2 steps cover the six possible run lengths).
 template <int D>
 AZ_HD uint64_t moves_dir(uint64_t P, uint64_t M) {
-  uint64_t fl = M & (P << D);
-  uint64_t fr = M & (P >> D);
-  fl |= M & (fl << D);
-  fr |= M & (fr >> D);
-  const uint64_t ml = M & (M << D);
-  const uint64_t mr = ml >> D;
-  fl |= ml & (fl << (2 * D));
-  fr |= mr & (fr >> (2 * D));
-  fl |= ml & (fl << (2 * D));
-  fr |= mr & (fr >> (2 * D));
-  return (fl << D) | (fr >> D);
+  using namespace tt;
+  uint64_t fl = M & shl<D>(P);
+  uint64_t fr = M & shr<D>(P);
+  fl = bop3<A | (B & C)>(fl, M, shl<D>(fl));
+  fr = bop3<A | (B & C)>(fr, M, shr<D>(fr));
+  const uint64_t ml = M & shl<D>(M);
+  const uint64_t mr = shr<D>(ml);
+  fl = bop3<A | (B & C)>(fl, ml, shl<2 * D>(fl));
+  fr = bop3<A | (B & C)>(fr, mr, shr<2 * D>(fr));
+  fl = bop3<A | (B & C)>(fl, ml, shl<2 * D>(fl));
+  fr = bop3<A | (B & C)>(fr, mr, shr<2 * D>(fr));
+  return shl<D>(fl) | shr<D>(fr);
+}
+
+// Horizontal moves by carry propagation: a run of opponent stones (columns 1..6, so no
+// run crosses a row end) starting just above an own stone is cleared by adding its first
+// stone, and the carry lands on the square past the run.  The downward direction is the
+// upward one on the 180-degree-rotated board.
+AZ_HD uint64_t moves_row_up(uint64_t P, uint64_t I) {
+  const uint64_t s = (P << 1) & I;
+  return (s + I) & ~I;  // landing squares (filtered by `empty` by the caller)
 }
 
 // Legal placements for `own` against `opp` (the rule of reference envs/othello.py:157-166).
 AZ_HD uint64_t legal(uint64_t own, uint64_t opp) {
+  using namespace tt;
   const uint64_t inner = opp & kInner;
-  uint64_t m = moves_dir<1>(own, inner);
-  m |= moves_dir<8>(own, opp);
-  m |= moves_dir<7>(own, inner);
-  m |= moves_dir<9>(own, inner);
-  return m & ~(own | opp);
+  const uint64_t row =
+      moves_row_up(own, inner) | rev64(moves_row_up(rev64(own), rev64(opp) & kInner));
+  const uint64_t m =
+      bop3<A | B | C>(row, moves_dir<8>(own, opp), moves_dir<7>(own, inner)) |
+      moves_dir<9>(own, inner);
+  return bop3<C & ~(A | B)>(own, opp, m);
+}
+
+// ---- capture set by ray masks ----------------------------------------------------------
+// Up-rays (towards higher bit indices, `sq` excluded) of the four lines through a square:
+// k = 0 row (+1), 1 column (+8), 2 diagonal (+9), 3 anti-diagonal (+7).  The down-rays of
+// sq are the up-rays of 63 - sq on the rotated board (rev64).
+AZ_HD uint64_t ray_up(int sq, int k) {
+  const int dr[4] = {0, 1, 1, 1}, dc[4] = {1, 0, 1, -1};
+  uint64_t m = 0;
+  int r = (sq >> 3) + dr[k], c = (sq & 7) + dc[k];
+  while (r < 8 && c >= 0 && c < 8) {
+    m |= 1ull << (r * 8 + c);
+    r += dr[k];
+    c += dc[k];
+  }
+  return m;
+}
+
+// Stones of `opp` captured along one up-ray R by a stone placed below it: the run of
+// opponent stones up to the first non-opponent square x, kept only if x holds an own stone.
+AZ_HD uint64_t ray_flips(uint64_t R, uint64_t own, uint64_t opp) {
+  using namespace tt;
+  const uint64_t o = R & ~opp;                     // non-opponent squares of the ray
+  const uint64_t d = o - 1ull;                     // bits below the first of them set
+  const uint64_t run = bop3<A & B & ~C>(R, d, o);  // the ray below x: all opponent stones
+  const uint64_t xo = bop3<A & ~B & C>(o, d, own); // x itself, if it holds an own stone
+  return xo ? run : 0ull;
+}
+
+// flips() from ray tables: `up` = the four up-rays of sq, `upr` = those of 63 - sq;
+// ownr / oppr = the rotated board.
+AZ_HD uint64_t flips_rays(const uint64_t* up, const uint64_t* upr, uint64_t own,
+                          uint64_t opp, uint64_t ownr, uint64_t oppr) {
+  const uint64_t fu = ray_flips(up[0], own, opp) | ray_flips(up[1], own, opp) |
+                      ray_flips(up[2], own, opp) | ray_flips(up[3], own, opp);
+  const uint64_t fd = ray_flips(upr[0], ownr, oppr) | ray_flips(upr[1], ownr, oppr) |
+                      ray_flips(upr[2], ownr, oppr) | ray_flips(upr[3], ownr, oppr);
+  return fu | rev64(fd);
 }
 
 // Stones captured along one line through `sq`: the ray above sq (towards higher bit
@@ -214,12 +326,55 @@ AZ_HD Move move(uint64_t own, uint64_t opp, int act) {
   return m;
 }
 
+// move() with the capture set from ray tables (`rays` = [64][4] up-rays, ray_up()).
+AZ_HD Move move_rays(const uint64_t* rays, uint64_t own, uint64_t opp, int act) {
+  Move m;
+  m.flags = 0;
+  m.illegal = false;
+  if (act == kPass) {
+    m.own = opp;
+    m.opp = own;
+    m.flags = kFlagPassed;
+    return m;
+  }
+  const int sq = act & 63;
+  const uint64_t nb = 1ull << sq;
+  const uint64_t cap =
+      flips_rays(rays + 4 * sq, rays + 4 * (63 - sq), own, opp, rev64(own), rev64(opp));
+  if ((unsigned)act > 64u || cap == 0ull || (nb & (own | opp))) {
+    m.own = own;
+    m.opp = opp;
+    m.illegal = true;
+    return m;
+  }
+  m.own = opp ^ cap;
+  m.opp = bop3<(tt::A | tt::B) ^ tt::C>(own, nb, cap);
+  return m;
+}
+
 // One board step for one position: placement or pass, then the next side's legal mask,
 // terminal check and disc difference.  Illegal placements leave the board unchanged and
 // set kFlagIllegal (the reference raises ValueError at envs/othello.py:419-421).
 AZ_HD Step step(uint64_t own, uint64_t opp, int act) {
   Step o;
   const Move m = move(own, opp, act);
+  o.own = m.own;
+  o.opp = m.opp;
+  if (m.illegal) {
+    o.legal = 0;
+    o.status = pack_status(kFlagIllegal, 0);
+    return o;
+  }
+  o.legal = legal(o.own, o.opp);
+  const int flags = m.flags | terminal_flags(o.own, o.opp, o.legal);
+  o.status = pack_status(flags, popc(o.own) - popc(o.opp));
+  return o;
+}
+
+// step() on the ray-table capture set (the batched entry points' formulation).
+AZ_HD Step step_rays(const uint64_t* rays, uint64_t own, uint64_t opp, int act) {
+  Step o;
+  const Move m = move_rays(rays, own, opp, act);
   o.own = m.own;
   o.opp = m.opp;
   if (m.illegal) {

@@ -32,10 +32,12 @@ int set_error(int code, const char* fmt, ...) {
 namespace {
 
 constexpr int kBlock = 256;
+static_assert(kBlock == 64 * 4, "k_step stages one up-ray per thread");
 
 // One position per lane per iteration, grid-stride.  Every global access is a
 // lane-contiguous 8-byte (own/opp/legal), 1-byte (act) or 2-byte (status) access, so a
-// wave moves 64 consecutive positions per instruction.
+// wave moves 64 consecutive positions per instruction.  The capture set comes from the
+// 2 KB up-ray table staged once per workgroup in LDS (two ds_read_b128 per ray set).
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ own,
                                                  const uint64_t* __restrict__ opp,
                                                  const uint8_t* __restrict__ act,
@@ -44,6 +46,9 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
                                                  uint64_t* __restrict__ legal_o,
                                                  uint16_t* __restrict__ status_o,
                                                  int64_t n) {
+  __shared__ __align__(16) uint64_t rays[64 * 4];
+  rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
+  __syncthreads();
   // every lane runs the same number of iterations (the terminal check is wave-cooperative)
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const int64_t n_pad = (n + kBlock - 1) / kBlock * kBlock;
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
       p = opp[i];
       a = act[i];
     }
-    const azb::Move mv = azb::move(o, p, a);
+    const azb::Move mv = azb::move_rays(rays, o, p, a);
     const bool ok = live && !mv.illegal;
     const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
     int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
@@ -88,6 +93,17 @@ __global__ __launch_bounds__(kBlock) void k_d4(const uint64_t* __restrict__ x,
     out[i] = azb::d4(x[i], sym[i] & 7);
 }
 
+// the same up-ray table on the host (built once, immutable afterwards)
+const uint64_t* host_rays() {
+  static const struct Table {
+    uint64_t r[64 * 4];
+    Table() {
+      for (int i = 0; i < 256; ++i) r[i] = azb::ray_up(i >> 2, i & 3);
+    }
+  } table;
+  return table.r;
+}
+
 unsigned grid_for(int64_t n) {
   // enough waves to cover the chip many times over; grid-stride for the rest
   const int64_t blocks = (n + kBlock - 1) / kBlock;
@@ -117,9 +133,10 @@ int oth_step_cpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_step_cpu: n=%lld < 0", (long long)n);
   AZ_REQUIRE(n == 0 || (own && opp && act && own_o && opp_o && legal_o && status_o),
              AZ_ERR_ARG, "oth_step_cpu: null buffer");
+  const uint64_t* rays = host_rays();
   int64_t first_bad = -1;
   for (int64_t i = 0; i < n; ++i) {
-    const azb::Step s = azb::step(own[i], opp[i], act[i]);
+    const azb::Step s = azb::step_rays(rays, own[i], opp[i], act[i]);
     own_o[i] = s.own;
     opp_o[i] = s.opp;
     legal_o[i] = s.legal;

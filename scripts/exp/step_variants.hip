@@ -276,11 +276,172 @@ __global__ __launch_bounds__(256) void v16(const uint64_t* own, const uint64_t* 
   }
 }
 
+
+// ---- r01b: ray-table capture set + bop3/carry legal (the product formulation) ----------
+#define RAYS __shared__ __align__(16) uint64_t rays[256]; if (threadIdx.x < 256) rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3); __syncthreads();
+// v17: plain per-lane step_rays (divergent terminal fill), grid-stride
+__global__ __launch_bounds__(256) void v17(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  GS { azb::Step s = azb::step_rays(rays, own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+}
+// v18: two positions per lane (i and i + n/2), loads of both issued first
+__global__ __launch_bounds__(256) void v18(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t h = n / 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < h; i += (int64_t)gridDim.x * 256) {
+    const uint64_t a0 = own[i], b0 = opp[i], a1 = own[i + h], b1 = opp[i + h];
+    const int c0 = act[i], c1 = act[i + h];
+    azb::Step s0 = azb::step_rays(rays, a0, b0, c0), s1 = azb::step_rays(rays, a1, b1, c1);
+    oo[i] = s0.own; po[i] = s0.opp; lo[i] = s0.legal; so[i] = s0.status;
+    oo[i + h] = s1.own; po[i + h] = s1.opp; lo[i + h] = s1.legal; so[i + h] = s1.status;
+  }
+}
+// v19: compute only (one store per lane at the end)
+__global__ __launch_bounds__(256) void v19(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t base_o = own[t & 32767], base_p = opp[t & 32767];
+  const int base_a = act[t & 32767];
+  uint64_t acc = 0;
+  for (int64_t i = t; i < n; i += (int64_t)gridDim.x * 256) {
+    azb::Step s = azb::step_rays(rays, base_o ^ acc, base_p, (base_a + (int)(i >> 20)) & 63);
+    acc ^= (s.own ^ s.opp ^ s.legal ^ s.status) & 1;
+  }
+  lo[t] = acc;
+}
+// v20: legal only, new formulation
+__global__ __launch_bounds__(256) void v20(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { lo[i] = azb::legal(own[i], opp[i]); }
+}
+// v21: product step with non-temporal stores
+__global__ __launch_bounds__(256) void v21(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  GS { azb::Step s = azb::step_rays(rays, own[i], opp[i], act[i]);
+    __builtin_nontemporal_store(s.own, oo + i); __builtin_nontemporal_store(s.opp, po + i);
+    __builtin_nontemporal_store(s.legal, lo + i); __builtin_nontemporal_store(s.status, so + i); }
+}
+
+// v22: v17 + next iteration's inputs prefetched into registers before this one's compute
+__global__ __launch_bounds__(256) void v22(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t a = 0, b = 0; int c = 0;
+  if (i < n) { a = own[i]; b = opp[i]; c = act[i]; }
+  for (; i < n; i += stride) {
+    const int64_t j = i + stride;
+    uint64_t a2 = 0, b2 = 0; int c2 = 0;
+    if (j < n) { a2 = __builtin_nontemporal_load(own + j); b2 = __builtin_nontemporal_load(opp + j); c2 = __builtin_nontemporal_load(act + j); }
+    azb::Step s = azb::step_rays(rays, a, b, c);
+    oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    a = a2; b = b2; c = c2;
+  }
+}
+// v23: prefetch distance 2
+__global__ __launch_bounds__(256) void v23(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t a = 0, b = 0, a1 = 0, b1 = 0; int c = 0, c1 = 0;
+  if (i < n) { a = own[i]; b = opp[i]; c = act[i]; }
+  if (i + stride < n) { a1 = own[i + stride]; b1 = opp[i + stride]; c1 = act[i + stride]; }
+  for (; i < n; i += stride) {
+    const int64_t j = i + 2 * stride;
+    uint64_t a2 = 0, b2 = 0; int c2 = 0;
+    if (j < n) { a2 = own[j]; b2 = opp[j]; c2 = act[j]; }
+    azb::Step s = azb::step_rays(rays, a, b, c);
+    oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    a = a1; b = b1; c = c1; a1 = a2; b1 = b2; c1 = c2;
+  }
+}
+// v24: v22 with plain loads
+__global__ __launch_bounds__(256) void v24(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t a = 0, b = 0; int c = 0;
+  if (i < n) { a = own[i]; b = opp[i]; c = act[i]; }
+  for (; i < n; i += stride) {
+    const int64_t j = i + stride;
+    uint64_t a2 = 0, b2 = 0; int c2 = 0;
+    if (j < n) { a2 = own[j]; b2 = opp[j]; c2 = act[j]; }
+    azb::Step s = azb::step_rays(rays, a, b, c);
+    oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    a = a2; b = b2; c = c2;
+  }
+}
+// v25: one block-tile of 1024 positions per iteration (4 per lane, strided by 256), loads of
+// the whole tile issued before any compute
+__global__ __launch_bounds__(256) void v25(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t tiles = n / 1024;
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t base = t * 1024 + threadIdx.x;
+    uint64_t a[4], b[4]; int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { a[k] = own[base + 256 * k]; b[k] = opp[base + 256 * k]; c[k] = act[base + 256 * k]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      azb::Step s = azb::step_rays(rays, a[k], b[k], c[k]);
+      const int64_t i = base + 256 * k;
+      oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status;
+    }
+  }
+}
+
+// v26: four consecutive positions per lane: 16-byte own/opp/out accesses, 4-byte act, 8-byte status
+__global__ __launch_bounds__(256) void v26(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t q = n / 4;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < q; j += (int64_t)gridDim.x * 256) {
+    const ulonglong2 a0 = reinterpret_cast<const ulonglong2*>(own)[2 * j], a1 = reinterpret_cast<const ulonglong2*>(own)[2 * j + 1];
+    const ulonglong2 b0 = reinterpret_cast<const ulonglong2*>(opp)[2 * j], b1 = reinterpret_cast<const ulonglong2*>(opp)[2 * j + 1];
+    const uint32_t c = reinterpret_cast<const uint32_t*>(act)[j];
+    azb::Step s0 = azb::step_rays(rays, a0.x, b0.x, c & 0xFF), s1 = azb::step_rays(rays, a0.y, b0.y, (c >> 8) & 0xFF);
+    azb::Step s2 = azb::step_rays(rays, a1.x, b1.x, (c >> 16) & 0xFF), s3 = azb::step_rays(rays, a1.y, b1.y, c >> 24);
+    reinterpret_cast<ulonglong2*>(oo)[2 * j] = make_ulonglong2(s0.own, s1.own); reinterpret_cast<ulonglong2*>(oo)[2 * j + 1] = make_ulonglong2(s2.own, s3.own);
+    reinterpret_cast<ulonglong2*>(po)[2 * j] = make_ulonglong2(s0.opp, s1.opp); reinterpret_cast<ulonglong2*>(po)[2 * j + 1] = make_ulonglong2(s2.opp, s3.opp);
+    reinterpret_cast<ulonglong2*>(lo)[2 * j] = make_ulonglong2(s0.legal, s1.legal); reinterpret_cast<ulonglong2*>(lo)[2 * j + 1] = make_ulonglong2(s2.legal, s3.legal);
+    reinterpret_cast<uint2*>(so)[j] = make_uint2((uint32_t)s0.status | ((uint32_t)s1.status << 16), (uint32_t)s2.status | ((uint32_t)s3.status << 16));
+  }
+}
+// v27: I/O only in v26's pattern
+__global__ __launch_bounds__(256) void v27(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const int64_t q = n / 4;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < q; j += (int64_t)gridDim.x * 256) {
+    const ulonglong2 a0 = reinterpret_cast<const ulonglong2*>(own)[2 * j], a1 = reinterpret_cast<const ulonglong2*>(own)[2 * j + 1];
+    const ulonglong2 b0 = reinterpret_cast<const ulonglong2*>(opp)[2 * j], b1 = reinterpret_cast<const ulonglong2*>(opp)[2 * j + 1];
+    const uint32_t c = reinterpret_cast<const uint32_t*>(act)[j];
+    reinterpret_cast<ulonglong2*>(oo)[2 * j] = make_ulonglong2(a0.x ^ c, a0.y); reinterpret_cast<ulonglong2*>(oo)[2 * j + 1] = a1;
+    reinterpret_cast<ulonglong2*>(po)[2 * j] = b0; reinterpret_cast<ulonglong2*>(po)[2 * j + 1] = b1;
+    reinterpret_cast<ulonglong2*>(lo)[2 * j] = make_ulonglong2(a0.x | b0.x, a0.y | b0.y); reinterpret_cast<ulonglong2*>(lo)[2 * j + 1] = make_ulonglong2(a1.x | b1.x, a1.y | b1.y);
+    reinterpret_cast<uint2*>(so)[j] = make_uint2(c, c >> 3);
+  }
+}
+// v28: I/O only, one position per lane, nontemporal stores
+__global__ __launch_bounds__(256) void v28(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  GS { uint64_t a = own[i], b = opp[i]; int c = act[i];
+    __builtin_nontemporal_store(a ^ c, oo + i); __builtin_nontemporal_store(b, po + i);
+    __builtin_nontemporal_store(a | b, lo + i); __builtin_nontemporal_store((uint16_t)c, so + i); }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16};
-  if (v < 0 || v > 16) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28};
+  if (v < 0 || v > 28) return -1;
   const int blk = v == 14 ? 64 : 256;
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -174,3 +174,27 @@ def test_get_training_data_matches_reference():
         traj = [(None, None, int(p), float(v)) for p, v in zip(r[:, 2], r[:, 3])]
         out = get_training_data(traj, int(r[0, 4]), float(r[0, 5]))
         assert np.array_equal(np.array([o[2] for o in out]), r[:, 6])
+
+
+def test_cpu_step_random_positions_vs_oracle():
+    """Unreachable dense/sparse positions and every action class (legal, occupied, no
+    capture, pass, out of range) against the C oracle: the ray-table capture set, the
+    carry/fill legal mask and the terminal flags hold on arbitrary boards, not only on the
+    corpus."""
+    from oracle import board as ob
+
+    rng = np.random.default_rng(7)
+    n = 1 << 17
+    cells = rng.integers(0, 3, size=(n, 64))
+    dense = rng.random(n) < 0.5  # half the boards sparse (mostly empty)
+    cells[~dense] = np.where(rng.random((int((~dense).sum()), 64)) < 0.8, 0,
+                             cells[~dense])
+    w = np.uint64(1) << np.arange(64, dtype=np.uint64)
+    own = np.bitwise_or.reduce(np.where(cells == 1, w, np.uint64(0)), axis=1)
+    opp = np.bitwise_or.reduce(np.where(cells == 2, w, np.uint64(0)), axis=1)
+    act = rng.integers(0, 70, size=n).astype(np.uint8)
+    o, p, lg, st = nat.step_cpu(own, opp, act, raise_illegal=False)
+    ro, rp, rl, rs, _ = ob.step_batch(own, opp, act)
+    assert (st == rs).all()
+    assert (o == ro).all() and (p == rp).all() and (lg == rl).all()
+    assert (nat.legal_cpu(own, opp) == ob.legal_batch(own, opp)).all()
