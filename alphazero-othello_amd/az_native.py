@@ -66,6 +66,8 @@ _I64 = ctypes.c_int64
 _U64 = ctypes.c_uint64
 _D = ctypes.c_double
 
+AZ_CONV_SPLIT3, AZ_CONV_FP16 = 0, 1  # az_conv3x3_mx_gpu modes
+
 # name -> argtypes (restype is int for every entry point except az_last_error)
 SIGNATURES = {
     "az_abi_version": [],
@@ -105,6 +107,8 @@ SIGNATURES = {
     "az_conv3x3_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P],
     "az_conv_stem_gpu": [_P, _P, _P, _P, _I32, _I32, _P],
     "az_conv3x3_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
+    "az_conv3x3_mx_prep_gpu": [_P, _P, _I32, _I32, _P],
+    "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
 }
 
 

@@ -146,22 +146,27 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
     load_a(s3, ra1);
   }
 
-  // ---- epilogue: D[row][col], col = lane&31, row = (k&3) + 8*(k>>2) + 4*(lane>>5)
+  // ---- epilogue: D[row][col], col = lane&31, row = (k&3) + 8*(k>>2) + 4*(lane>>5); a
+  // 32-row tile lies inside one board, so the tail-board test is uniform per tile
 #pragma unroll
-  for (int ni = 0; ni < G::TN; ++ni) {
-    const int co = col0 + 32 * ni + r;
-    const float bv = bias[co];
+  for (int mi = 0; mi < G::TM; ++mi) {
+    if (((row0 + 32 * mi) >> 6) >= nb) continue;
 #pragma unroll
-    for (int mi = 0; mi < G::TM; ++mi) {
+    for (int ni = 0; ni < G::TN; ++ni) {
+      const int co = col0 + 32 * ni + r;
+      const float bv = bias[co];
+      const size_t o0 = ((size_t)b0 * 64 + row0 + 32 * mi + 4 * h) * C + co;
+      float rv[16];
+      if (RES) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rv[k] = res[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C];
+      }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int m = row0 + 32 * mi + (k & 3) + 8 * (k >> 2) + 4 * h;
-        if ((m >> 6) >= nb) continue;
-        const size_t o = ((size_t)b0 * 64 + m) * C + co;
         float v = acc[mi][ni][k] + bv;
-        if (RES) v += res[o];
+        if (RES) v += rv[k];
         if (RELU) v = fmaxf(v, 0.0f);
-        y[o] = v;
+        y[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C] = v;
       }
     }
   }

@@ -268,6 +268,21 @@ int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* bias, const
                        float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t cfg,
                        void* stream);
 
+/* The same convolution on the 16-bit MFMA pipe (csrc/conv16.hip).  mode:
+ *   AZ_CONV_SPLIT3 — fp32-accurate: each fp32 operand split into three bf16 words, the six
+ *                    leading partial products accumulated in fp32 (error at fp32's own
+ *                    rounding unit; tests/test_nn_gpu.py measures it against fp64);
+ *   AZ_CONV_FP16   — one fp16 product (BASELINE configs[4], fp16 inference).
+ * wq: the weights re-laid by az_conv3x3_mx_prep_gpu from w9 [9][Co][Ci] fp32 into
+ * [9][Ci/16][planes][Co][16] 16-bit words (planes = 3 for SPLIT3, 1 for FP16; 16-byte
+ * aligned, 9*C*C*planes*2 bytes).  Replaces the same reference layers as az_conv3x3_gpu. */
+enum { AZ_CONV_SPLIT3 = 0, AZ_CONV_FP16 = 1 };
+int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t mode,
+                           void* stream);
+int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias, const float* res,
+                      float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t mode,
+                      void* stream);
+
 /* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
  * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,
  * 186-187). */

@@ -87,3 +87,65 @@ def test_inference_copy_matches_module(kind, conv):
         p, val = fused.evaluate_planes(x)
     torch.testing.assert_close(p, p_ref, atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
+
+
+def _mx_conv(x, w, b, r, relu, mode):
+    C = x.shape[1]
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
+    wq = torch.empty(9 * C * C * planes, dtype=torch.int16, device="cuda")
+    nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode, nat.stream_ptr()),
+              "az_conv3x3_mx_prep_gpu")
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_mx_gpu(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
+                                        None if r is None else nat.ptr(r), nat.ptr(y), x.shape[0],
+                                        C, int(relu), mode, nat.stream_ptr()), "az_conv3x3_mx_gpu")
+    torch.cuda.synchronize()
+    return y
+
+
+def _case(C, B, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, C, 8, 8, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(C, generator=g)
+    r = torch.randn(B, C, 8, 8, generator=g)
+    cl = lambda t: t.cuda().contiguous(memory_format=torch.channels_last)
+    ref64 = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    return cl(x), w.cuda(), b.cuda(), cl(r), ref64
+
+
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("B", [1, 3, 130])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_conv3x3_split3_is_fp32_accurate(C, B, res, relu):
+    """The bf16x3-split MFMA conv against an fp64 reference: its error must stay at the fp32
+    MFMA kernel's level (max |err| <= 2x the fp32 kernel's + 1e-6, mean <= 2x), and within
+    the fp32 tolerance of this file against torch fp32."""
+    x, w, b, r, ref64 = _case(C, B, C * 13 + B)
+    rr = r if res else None
+    y = _mx_conv(x, w, b, rr, relu, nat.AZ_CONV_SPLIT3)
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    y32 = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
+                                     nat.ptr(y32), B, C, int(relu), nat.stream_ptr()), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ref = ref64 + (r.cpu().double() if res else 0)
+    if relu:
+        ref = F.relu(ref)
+    e_mx = (y.cpu().double() - ref).abs()
+    e_32 = (y32.cpu().double() - ref).abs()
+    assert e_mx.max() <= 2 * e_32.max() + 1e-6, (e_mx.max(), e_32.max())
+    assert e_mx.mean() <= 2 * e_32.mean() + 1e-8, (e_mx.mean(), e_32.mean())
+    torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv3x3_fp16_mode(C, res):
+    """fp16 inference (configs[4]): fp16 operands, fp32 accumulation; tolerance of fp16
+    rounding of both operands over K = 9C terms."""
+    x, w, b, r, ref64 = _case(C, 37, C + 5)
+    y = _mx_conv(x, w, b, r if res else None, True, nat.AZ_CONV_FP16)
+    ref = F.relu(ref64 + (r.cpu().double() if res else 0)).float().cuda()
+    torch.testing.assert_close(y, ref, atol=5e-3, rtol=5e-3)
