@@ -33,9 +33,9 @@ class Inference:
         float32 [B, 65], tanh values float32 [B])."""
         n = getattr(self, "board_size", 3 if planes.shape[-1] == 9 else 8)
         x = planes.view(planes.shape[0], 1, n, n)
-        p = next(self.parameters())
-        if x.dtype != p.dtype:
-            x = x.to(p.dtype)
+        dt = getattr(self, "input_dtype", None) or next(self.parameters()).dtype
+        if x.dtype != dt:
+            x = x.to(dt)
         logits, value = self(x)
         return (torch.softmax(logits.float(), dim=-1),
                 value.float().reshape(-1))
@@ -149,12 +149,22 @@ def get_config(net):
 
 
 def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
-                   conv="hip") -> nn.Module:
+                   conv="hip", precision=None) -> nn.Module:
     """An eval-mode copy of `net` on `device` for the batched engine: BatchNorm folded
     into the preceding convolution (same function in eval mode, fewer kernels per step).
-    With `fused` (fp32, AlphaZeroNet / FastOthelloNet) the convolutions run without bias
-    and one HIP epilogue kernel applies bias + residual + ReLU (csrc/nn_fused.hip).
-    `dtype` float16 is config #5's fp16 inference."""
+    With `fused` (AlphaZeroNet / FastOthelloNet) the convolutions run without bias and one
+    HIP epilogue applies bias + residual + ReLU.  conv="hip" runs the 3x3 trunk on the
+    fused MFMA kernels, in `precision`:
+      "split3" (default for fp32): bf16x3-split operands on the 16-bit MFMA pipe, six
+               partial products accumulated in fp32 — fp32-accurate (csrc/conv16.hip;
+               tests/test_nn_gpu.py bounds its error by the fp32 kernel's against fp64);
+      "fp32":  fp32 MFMA (csrc/conv.hip);
+      "fp16":  fp16 operands, fp32 accumulation (config #5's fp16 inference; the default
+               when dtype is float16).
+    Activations, the stem and the heads stay fp32 on the fused path."""
+    if precision is None:
+        precision = "fp16" if dtype == torch.float16 else "split3"
+    assert precision in ("split3", "fp32", "fp16"), precision
     import copy
 
     m = copy.deepcopy(net).eval()
@@ -178,10 +188,11 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
         if isinstance(mod, FastOthelloNet):
             for seq in (mod.initial_conv, mod.conv_add):
                 seq[1] = fold(seq[0], seq[1])
-    m = m.to(device=device, dtype=dtype)
+    fusable = fused and isinstance(m, (AlphaZeroNet, FastOthelloNet))
+    m = m.to(device=device, dtype=torch.float32 if fusable else dtype)
     m = m.to(memory_format=torch.channels_last)
-    if fused and dtype == torch.float32 and isinstance(m, (AlphaZeroNet, FastOthelloNet)):
-        return FusedInferenceNet(m, conv=conv).eval()
+    if fusable:
+        return FusedInferenceNet(m, conv=conv, precision=precision).eval()
     return m.eval()
 
 
@@ -211,18 +222,32 @@ class _ConvEpilogue(nn.Module):
 
 
 class _HipConv3x3(nn.Module):
-    """3x3 conv (Ci = Co in {64, 128}) + bias (+ residual) + ReLU in one fp32 MFMA kernel
-    (csrc/conv.hip); weights re-laid [tap][Co][Ci]."""
+    """3x3 conv (Ci = Co in {64, 128}) + bias (+ residual) + ReLU in one MFMA kernel:
+    precision "fp32" = csrc/conv.hip (weights re-laid [tap][Co][Ci]); "split3" / "fp16" =
+    csrc/conv16.hip (weights split once into 16-bit planes by az_conv3x3_mx_prep_gpu)."""
 
-    def __init__(self, conv: nn.Conv2d):
+    MODES = {"split3": 0, "fp16": 1}  # AZ_CONV_SPLIT3, AZ_CONV_FP16
+
+    def __init__(self, conv: nn.Conv2d, precision="split3"):
         super().__init__()
+        import az_native as nat
+
         w = conv.weight.detach()
         co, ci = w.shape[0], w.shape[1]
         assert co == ci and co in (64, 128) and w.shape[2:] == (3, 3)
         self.channels = co
-        self.w9 = nn.Parameter(w.permute(2, 3, 0, 1).reshape(9, co, ci).contiguous(),
-                               requires_grad=False)
+        self.precision = precision
+        w9 = w.float().permute(2, 3, 0, 1).reshape(9, co, ci).contiguous()
         self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
+        if precision == "fp32":
+            self.w9 = nn.Parameter(w9, requires_grad=False)
+        else:
+            self.mode = self.MODES[precision]
+            planes = 3 if precision == "split3" else 1
+            wq = torch.empty(9 * co * ci * planes, dtype=torch.int16, device=w.device)
+            nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(wq), co, self.mode,
+                                                     nat.stream_ptr()), "az_conv3x3_mx_prep_gpu")
+            self.wq = nn.Parameter(wq, requires_grad=False)
 
     def forward(self, x, res=None, relu=True):
         import az_native as nat
@@ -231,10 +256,17 @@ class _HipConv3x3(nn.Module):
         if res is not None:
             res = res.contiguous(memory_format=torch.channels_last)
         y = torch.empty_like(x, memory_format=torch.channels_last)
-        nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(self.w9), nat.ptr(self.bias),
-                                         None if res is None else nat.ptr(res), nat.ptr(y),
-                                         x.shape[0], self.channels, int(relu),
-                                         nat.stream_ptr()), "az_conv3x3_gpu")
+        rp = None if res is None else nat.ptr(res)
+        if self.precision == "fp32":
+            rc = nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(self.w9), nat.ptr(self.bias), rp,
+                                        nat.ptr(y), x.shape[0], self.channels, int(relu),
+                                        nat.stream_ptr())
+            nat.check(rc, "az_conv3x3_gpu")
+        else:
+            rc = nat.lib.az_conv3x3_mx_gpu(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp,
+                                           nat.ptr(y), x.shape[0], self.channels, int(relu),
+                                           self.mode, nat.stream_ptr())
+            nat.check(rc, "az_conv3x3_mx_gpu")
         return y
 
 
@@ -271,16 +303,23 @@ def _merge_1x1(a: nn.Conv2d, b: nn.Conv2d) -> nn.Conv2d:
 class FusedInferenceNet(nn.Module, Inference):
     """Inference-only form of AlphaZeroNet / FastOthelloNet with BatchNorm folded and every
     conv epilogue fused (same function as the source net in eval mode).  conv="hip": the
-    stem and the 3x3 trunk run on the fused MFMA kernels of csrc/conv.hip; conv="miopen":
-    MIOpen convolutions + the az_bias_act_gpu epilogue."""
+    stem and the 3x3 trunk run on the fused MFMA kernels of csrc/conv.hip (stem, fp32 trunk)
+    and csrc/conv16.hip (split3 / fp16 trunk); conv="miopen": MIOpen convolutions + the
+    az_bias_act_gpu epilogue."""
 
-    def __init__(self, m: nn.Module, conv="hip"):
+    input_dtype = torch.float32
+
+    def __init__(self, m: nn.Module, conv="hip", precision="split3"):
         super().__init__()
         self.conv_impl = conv
+        self.precision = precision
         self.kind = "az" if isinstance(m, AlphaZeroNet) else "fast"
         self.board_size = m.board_size
         self.softmax = nn.Softmax(dim=-1)
-        C3 = _HipConv3x3 if conv == "hip" else _ConvEpilogue
+        if conv == "hip":
+            C3 = lambda c: _HipConv3x3(c, precision)  # noqa: E731
+        else:
+            C3 = _ConvEpilogue
         Stem = _HipStem if conv == "hip" else _ConvEpilogue
         if self.kind == "az":
             self.stem = Stem(m.conv0)

@@ -14,86 +14,98 @@
 //   AZ_CONV_FP16: one fp16 product (BASELINE configs[4]'s fp16 inference).
 //
 // GEMM view: M = B*64 output positions, N = C, K = 9 taps x C.  Workgroup = 2 boards
-// (M = 128) x all C columns, waves 2 (M) x C/64 (N), each wave 64 x 64 (2 x 2 tiles of
-// 32x32).  The two input boards sit in LDS as fp32 for the whole kernel (positions padded
-// to C + 4 floats: conflict-free ds_read_b128 row gathers; one all-zero position for the
-// off-board taps); A fragments are split into bf16 words in registers.  Weights arrive
-// pre-split from az_conv3x3_mx_prep_gpu as [tap][ci/16][plane][co][16] 16-bit words: each
-// (tap, 16-channel chunk) step is one contiguous PLANES*C*32-byte block, loaded by the
-// workgroup two steps ahead into registers and stored into a double-buffered LDS stage
-// (rows padded to 48 B: conflict-free ds_read_b128), one barrier per step.
+// (M = 128 rows) x all C columns; wave w owns all 128 rows x columns 32w..32w+31 (4 x 1
+// tiles of 32x32), so each weight fragment feeds four MFMAs.
+//   * A: the two boards are split into PLANES 16-bit words per element ONCE, while being
+//     staged into LDS as [position][plane][C] (+16 B per position: conflict-free
+//     ds_read_b128 row gathers; one all-zero position for the off-board taps), and stay
+//     resident for all 9 taps.
+//   * B: weights pre-split by az_conv3x3_mx_prep_gpu into [tap][ci/16][plane][Co][16]
+//     words; every wave streams its own 32 columns straight from L2 into registers, three
+//     (tap, 16-channel) steps ahead.  No LDS stage, so the main loop has no barrier.
+//   * A fragments of the next step are read from LDS during this step's MFMAs.
+//   * Epilogue straight from the accumulators: + bias, + residual, ReLU, NHWC store.
 #include <type_traits>
 
 #include "common.h"
+
+// experiment hooks (scripts/exp/conv16_exp.py builds copies with bits set): 1 = no A reads
+// in the main loop, 2 = no weight loads in the main loop, 4 = no board staging, 8 = no
+// epilogue stores.  The product build leaves it 0.
+#ifndef AZ_MX_EXP
+#define AZ_MX_EXP 0
+#endif
 
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 template <int C_, int MODE_>
 struct Mx {
   static constexpr int C = C_, MODE = MODE_;
   static constexpr int PLANES = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
   static constexpr int BOARDS = 2;
-  static constexpr int WAVES_N = C / 64, WAVES = 2 * WAVES_N, THREADS = 64 * WAVES;
-  static constexpr int TM = 2, TN = 2;
-  static constexpr int APOS = PLANES * C * 2 + 16;  // bytes per staged position (padded)
+  static constexpr int TM = 4;                      // 32-row tiles per wave (= 128 rows)
+  static constexpr int WAVES = C / 32, THREADS = 64 * WAVES;
+  static constexpr int APOS = PLANES * C * 2 + 16;  // LDS bytes per staged position
   static constexpr int A_BYTES = (BOARDS * 64 + 1) * APOS;
-  static constexpr int BROW = 48;                   // bytes per (plane, co) row of a stage
-  static constexpr int BSTAGE = PLANES * C * BROW;  // bytes per LDS stage
   static constexpr int CHUNKS = C / 16, STEPS = 9 * CHUNKS;
-  static constexpr int STEP_BYTES = PLANES * C * 32;  // global bytes per step
-  static constexpr int LOADS = STEP_BYTES / (THREADS * 16);
-  static constexpr size_t LDS_BYTES = (size_t)A_BYTES + 2 * BSTAGE;
-  static_assert(LOADS == PLANES, "one 16-byte load per plane per thread per step");
+  static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes per (tap, chunk) step
+  static constexpr size_t LDS_BYTES = A_BYTES;
+  static_assert(STEPS % 6 == 0, "the main loop is unrolled by 6");
 };
 
-
-// MFMA operands of one step: PLANES 16-bit words per element for A and for B
 template <class G>
-struct Frags {
-  using T = typename std::conditional<G::MODE == AZ_CONV_SPLIT3, bf16x8, f16x8>::type;
-  T a[G::PLANES][G::TM];
-  T b[G::PLANES][G::TN];
+using Word8 = typename std::conditional<G::MODE == AZ_CONV_SPLIT3, bf16x8, f16x8>::type;
+
+template <class G>
+struct AFrag {
+  Word8<G> v[G::PLANES][G::TM];
+};
+template <class G>
+struct BFrag {
+  Word8<G> v[G::PLANES];
 };
 
-// one step's A fragments: lane (r, h) of tile mi reads, per plane, the 8 words of channels
+// A fragments of step s: lane (r, h) of tile mi reads, per plane, the 8 words of channels
 // ci0+8h.. of its row's tapped position (or of the all-zero position)
 template <class G>
-__device__ __forceinline__ void mx_read_a(Frags<G>& f, const char* lds_a, int s,
+__device__ __forceinline__ void mx_read_a(AFrag<G>& f, const char* lds_a, int s,
                                           const int (&pos0)[G::TM], const int (&ok9)[G::TM],
                                           int h) {
-  using T = typename Frags<G>::T;
   const int tap = s / G::CHUNKS, ci0 = (s % G::CHUNKS) * 16;
   const int d = (tap / 3 - 1) * 8 + (tap % 3 - 1);
+  const char* p[G::TM];
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi) {
     const int pos = (ok9[mi] >> tap) & 1 ? pos0[mi] + d : G::BOARDS * 64;
-    const char* p = lds_a + pos * G::APOS + (ci0 + 8 * h) * 2;
-#pragma unroll
-    for (int pl = 0; pl < G::PLANES; ++pl)
-      f.a[pl][mi] = *reinterpret_cast<const T*>(p + pl * G::C * 2);
+    p[mi] = lds_a + pos * G::APOS + (ci0 + 8 * h) * 2;
   }
+  // issued in the order mx_mma consumes them: the last plane (x2) first
+#pragma unroll
+  for (int pl = G::PLANES - 1; pl >= 0; --pl)
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi)
+      f.v[pl][mi] = *reinterpret_cast<const Word8<G>*>(p[mi] + pl * G::C * 2);
+}
+
+// B fragments of step s: this lane's 16 bytes of each plane (column col0 + r, k = 8h..)
+template <class G>
+__device__ __forceinline__ void mx_load_b(BFrag<G>& f, const char* wlane, int s) {
+#pragma unroll
+  for (int pl = 0; pl < G::PLANES; ++pl)
+    f.v[pl] = *reinterpret_cast<const Word8<G>*>(wlane + (size_t)s * G::STEP_BYTES +
+                                                 pl * G::C * 32);
 }
 
 template <class G>
-__device__ __forceinline__ void mx_read_b(Frags<G>& f, const char* stage, const int (&boff)[G::TN]) {
-  using T = typename Frags<G>::T;
-#pragma unroll
-  for (int p = 0; p < G::PLANES; ++p)
-#pragma unroll
-    for (int ni = 0; ni < G::TN; ++ni)
-      f.b[p][ni] = *reinterpret_cast<const T*>(stage + p * G::C * G::BROW + boff[ni]);
-}
-
-template <class G>
-__device__ __forceinline__ void mx_mma(f32x16 (&acc)[G::TM][G::TN], const Frags<G>& f) {
+__device__ __forceinline__ void mx_mma(f32x16 (&acc)[G::TM], const AFrag<G>& a,
+                                       const BFrag<G>& b) {
   if constexpr (G::MODE == AZ_CONV_SPLIT3) {
     // smallest partial products first (x2y0, x1y1, x0y2, x1y0, x0y1, x0y0); consecutive
     // MFMAs write different accumulators
@@ -102,36 +114,35 @@ __device__ __forceinline__ void mx_mma(f32x16 (&acc)[G::TM][G::TN], const Frags<
     for (int t = 0; t < 6; ++t)
 #pragma unroll
       for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < G::TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[PA[t]][mi], f.b[PB[t]][ni],
-                                                                acc[mi][ni], 0, 0, 0);
+        acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[PA[t]][mi], b.v[PB[t]], acc[mi],
+                                                          0, 0, 0);
   } else {
 #pragma unroll
     for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < G::TN; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[0][mi], f.b[0][ni], acc[mi][ni],
-                                                             0, 0, 0);
+      acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0][mi], b.v[0], acc[mi], 0, 0, 0);
   }
 }
 
+// issue pattern of one main-loop step (see AZ_MX_STEP)
 template <class G>
-__device__ __forceinline__ void mx_load_w(u32x4 (&wr)[G::LOADS], const u32x4* wsrc, int s) {
+__device__ __forceinline__ void mx_sched() {
+  constexpr int kMfma = (G::MODE == AZ_CONV_SPLIT3 ? 6 : 1) * G::TM;
+  constexpr int kDs = G::PLANES * G::TM;
+  __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);  // VALU (addresses)
+  constexpr int kPer = kMfma / kDs > 0 ? kMfma / kDs : 1;
 #pragma unroll
-  for (int k = 0; k < G::LOADS; ++k)
-    wr[k] = wsrc[(size_t)s * (G::STEP_BYTES / 16) + k * G::THREADS];
-}
-template <class G>
-__device__ __forceinline__ void mx_store_w(const u32x4 (&wr)[G::LOADS], char* stage,
-                                           const int (&bdst)[G::LOADS]) {
-#pragma unroll
-  for (int k = 0; k < G::LOADS; ++k) *reinterpret_cast<u32x4*>(stage + bdst[k]) = wr[k];
+  for (int i = 0; i < kDs; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, kPer, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // DS read
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, kMfma, 0);   // remaining MFMAs
+  __builtin_amdgcn_sched_group_barrier(0x020, G::PLANES, 0);  // VMEM read
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <class G, bool RES, bool RELU>
 __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restrict__ x,
-                                                           const u32x4* __restrict__ wq,
+                                                           const char* __restrict__ wq,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ res,
                                                            float* __restrict__ y,
@@ -139,24 +150,20 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   constexpr int C = G::C, kBoards = G::BOARDS, kThreads = G::THREADS;
   extern __shared__ float4 lds4[];
   char* lds_a = reinterpret_cast<char*>(lds4);
-  char* lds_b = lds_a + G::A_BYTES;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int col0 = wave * 32;
   const int b0 = blockIdx.x * kBoards;
   const int nb = n_boards - b0 < kBoards ? n_boards - b0 : kBoards;
+  constexpr int last = G::STEPS - 1;
 
-  // ---- weights: this thread's share of one step (LOADS x 16 B) and its LDS slots
-  const u32x4* wsrc = wq + tid;
-  int bdst[G::LOADS];
-#pragma unroll
-  for (int k = 0; k < G::LOADS; ++k) {
-    const int idx = k * kThreads + tid;  // 16-byte unit within the step block
-    const int plane = idx / (2 * C), rem = idx % (2 * C);
-    bdst[k] = plane * C * G::BROW + (rem >> 1) * G::BROW + (rem & 1) * 16;
-  }
-  u32x4 wx[G::LOADS], wy[G::LOADS];
-  mx_load_w<G>(wx, wsrc, 0);
-  mx_load_w<G>(wy, wsrc, 1);
+  // weights of the first three steps are in flight while the boards are staged
+  const char* wlane = wq + (size_t)(col0 + r) * 32 + h * 16;
+  BFrag<G> b0f, b1f, b2f;
+  mx_load_b<G>(b0f, wlane, 0);
+  mx_load_b<G>(b1f, wlane, 1);
+  mx_load_b<G>(b2f, wlane, 2);
 
   // ---- stage the input boards (NHWC) into LDS as PLANES 16-bit words per element (the
   // split of every activation done once here, not once per tap); zero-fill a missing tail
@@ -164,7 +171,7 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   {
     constexpr int V = (kBoards * 64 + 1) * C / 4;
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
-    for (int v = tid; v < V; v += kThreads) {
+    for (int v = tid; v < ((AZ_MX_EXP & 4) ? 0 : V); v += kThreads) {
       const int pos = v / (C / 4), c4 = v % (C / 4);
       float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
       if (pos < nb * 64) val = src[v];
@@ -183,18 +190,13 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
       }
     }
   }
-  mx_store_w<G>(wx, lds_b, bdst);
-  mx_load_w<G>(wx, wsrc, 2);
   __syncthreads();
 
-  const int wm = wave / G::WAVES_N, wn = wave % G::WAVES_N;
-  const int row0 = wm * 64, col0 = wn * 64;
-  const int r = lane & 31, h = lane >> 5;
   // per A tile: this lane's output position and which of the 9 taps land on the board
   int pos0[G::TM], ok9[G::TM];
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi) {
-    const int m = row0 + 32 * mi + r;
+    const int m = 32 * mi + r;
     const int py = (m >> 3) & 7, px = m & 7;
     pos0[mi] = m;
     int ok = 0;
@@ -205,62 +207,63 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
     }
     ok9[mi] = ok;
   }
-  int boff[G::TN];
-#pragma unroll
-  for (int ni = 0; ni < G::TN; ++ni) boff[ni] = (col0 + 32 * ni + r) * G::BROW + h * 16;
 
-  f32x16 acc[G::TM][G::TN];
+  f32x16 acc[G::TM];
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < G::TN; ++ni)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc[mi][ni][k] = 0.0f;
+    for (int k = 0; k < 16; ++k) acc[mi][k] = 0.0f;
 
-  // Two LDS weight stages, one barrier per step; the next step's A fragments are read
-  // from the resident boards before this step's MFMAs; weights are loaded two steps ahead
-  // into registers.  Every load and store is unconditional (indices clamped to the last
-  // step; surplus stores land in a stage nobody reads again), which keeps the compiler's
-  // vmcnt bookkeeping exact.
-  static_assert(G::STEPS % 2 == 0 && G::STEPS >= 4, "step pairs");
-  constexpr int last = G::STEPS - 1;
-  Frags<G> f0, f1;
-  mx_read_a<G>(f0, lds_a, 0, pos0, ok9, h);
-  for (int s = 0; s < G::STEPS; s += 2) {
-    mx_read_a<G>(f1, lds_a, s + 1, pos0, ok9, h);
-    mx_read_b<G>(f0, lds_b, boff);
-    mx_mma<G>(acc, f0);
-    mx_store_w<G>(wy, lds_b + G::BSTAGE, bdst);
-    mx_load_w<G>(wy, wsrc, s + 3 < last ? s + 3 : last);
-    __syncthreads();
-    mx_read_a<G>(f0, lds_a, s + 2 < last ? s + 2 : last, pos0, ok9, h);
-    mx_read_b<G>(f1, lds_b + G::BSTAGE, boff);
-    mx_mma<G>(acc, f1);
-    mx_store_w<G>(wx, lds_b, bdst);
-    mx_load_w<G>(wx, wsrc, s + 4 < last ? s + 4 : last);
-    __syncthreads();
+  // Step s: MFMAs on A set s%2 and B set s%3; then B set s%3 is reloaded with step s+3 and
+  // A set (s+1)%2 read for step s+1.  Indices are clamped to the last step so every load
+  // is unconditional (exact vmcnt bookkeeping); the surplus loads are never consumed.
+  AFrag<G> a0f, a1f;
+  mx_read_a<G>(a0f, lds_a, 0, pos0, ok9, h);
+  // The machine scheduler would put a step's loads in one burst ahead of its MFMAs (the
+  // MFMA pipe then idles while they issue) or sink them behind; sched_group_barrier pins
+  // the issue pattern: address VALU first, then each LDS read of the next step's A in the
+  // shadow of two MFMAs, then the weight loads behind the MFMAs that consume their
+  // registers.
+#define AZ_MX_STEP(S, AC, AN, BC)                                                 \
+  {                                                                               \
+    const int s_ = (S);                                                           \
+    if (!(AZ_MX_EXP & 1))                                                         \
+      mx_read_a<G>(AN, lds_a, s_ + 1 < last ? s_ + 1 : last, pos0, ok9, h);       \
+    mx_mma<G>(acc, AC, BC);                                                       \
+    if (!(AZ_MX_EXP & 2)) mx_load_b<G>(BC, wlane, s_ + 3 < last ? s_ + 3 : last); \
+    mx_sched<G>();                                                                \
   }
+  for (int s = 0; s < G::STEPS; s += 6) {
+    AZ_MX_STEP(s + 0, a0f, a1f, b0f)
+    AZ_MX_STEP(s + 1, a1f, a0f, b1f)
+    AZ_MX_STEP(s + 2, a0f, a1f, b2f)
+    AZ_MX_STEP(s + 3, a1f, a0f, b0f)
+    AZ_MX_STEP(s + 4, a0f, a1f, b1f)
+    AZ_MX_STEP(s + 5, a1f, a0f, b2f)
+  }
+#undef AZ_MX_STEP
 
   // ---- epilogue: D[row][col], col = lane&31, row = (k&3) + 8*(k>>2) + 4*(lane>>5); a
   // 32-row tile lies inside one board, so the tail-board test is uniform per tile
+  const int co = col0 + r;
+  const float bv = bias[co];
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi) {
-    if (((row0 + 32 * mi) >> 6) >= nb) continue;
+    if (((32 * mi) >> 6) >= nb) continue;
+    const size_t o0 = ((size_t)b0 * 64 + 32 * mi + 4 * h) * C + co;
+    float rv[16];
+    if (RES) {
 #pragma unroll
-    for (int ni = 0; ni < G::TN; ++ni) {
-      const int co = col0 + 32 * ni + r;
-      const float bv = bias[co];
-      const size_t o0 = ((size_t)b0 * 64 + row0 + 32 * mi + 4 * h) * C + co;
-      float rv[16];
-      if (RES) {
+      for (int k = 0; k < 16; ++k) rv[k] = res[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C];
+    }
 #pragma unroll
-        for (int k = 0; k < 16; ++k) rv[k] = res[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C];
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        float v = acc[mi][ni][k] + bv;
-        if (RES) v += rv[k];
-        if (RELU) v = fmaxf(v, 0.0f);
+    for (int k = 0; k < 16; ++k) {
+      float v = acc[mi][k] + bv;
+      if (RES) v += rv[k];
+      if (RELU) v = fmaxf(v, 0.0f);
+      if (AZ_MX_EXP & 8) {
+        if (v == 12345.f) y[o0] = v;
+      } else {
         y[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C] = v;
       }
     }
@@ -306,7 +309,7 @@ int launch_mx(const float* x, const void* wq, const float* bias, const float* re
                                  (int)G::LDS_BYTES));
     attr_set = true;
   }
-  const u32x4* w = static_cast<const u32x4*>(wq);
+  const char* w = static_cast<const char*>(wq);
   const dim3 blk(G::THREADS);
   const size_t lds = G::LDS_BYTES;
   if (res && relu)

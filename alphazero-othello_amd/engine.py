@@ -246,14 +246,15 @@ class BatchedSelfPlay:
 
     `net` is any module with the reference forward signature ([B,1,8,8] -> (logits [B,65],
     value [B,1])); it is evaluated through `Models.inference_copy` (BatchNorm folded,
-    channels-last, optional fp16 = config #5).  `args` uses the reference's keys
+    channels-last, trunk `precision` "split3" (fp32-accurate, default) / "fp32" / "fp16" =
+    config #5).  `args` uses the reference's keys
     (train.py:399-423): c_puct, num_simulations, dirichlet_alpha, dirichlet_epsilon,
     mcts_temperature, num_exploratory_moves, lambda.
     """
 
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
-                 device=None, fold=True, steps_per_graph=8):
+                 device=None, fold=True, steps_per_graph=8, precision=None):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -270,7 +271,7 @@ class BatchedSelfPlay:
         if net is None:
             self.net = None
         elif fold:
-            self.net = inference_copy(net, self.device, dtype)
+            self.net = inference_copy(net, self.device, dtype, precision=precision)
         else:
             self.net = net.to(self.device).eval()
         self.use_graph = use_graph

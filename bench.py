@@ -7,7 +7,10 @@ Workload (BASELINE.json configs[2], the one the metric is quoted on): 8x8 Othell
 400 sims/move, AlphaZeroNet(8, 65, 5, 128) random init (no checkpoints offline), leaf batch
 1,024 = 1,024 concurrent games per GPU with one leaf each per step; the reference's
 self-play settings (train.py:399-423): c_puct 2, Dirichlet alpha 1 / eps 0.3 at the root,
-temperature 1 for 35 plies then 0, lambda 0.98.  fp32 throughout (the reference's dtype).
+temperature 1 for 35 plies then 0, lambda 0.98.  The net is fp32-accurate: the 3x3 trunk runs
+fp32 operands split into three bf16 words on the 16-bit MFMA pipe with fp32 accumulation
+(error bounded by the fp32 MFMA kernel's, tests/test_nn_gpu.py); --conv-precision fp32
+selects the plain fp32 MFMA kernel.
 
 A step is one batched simulation over every game slot: select (descent + leaf pack) ->
 net forward -> expand+backup -> move phase; games restart as they finish (weak scaling:
@@ -48,6 +51,14 @@ SELFPLAY_ARGS = {"c_puct": 2.0, "num_simulations": 400, "dirichlet_alpha": 1.0,
 REF_PLIES_PER_GAME = 60.0  # SURVEY.md 6 (measured on the reference at 400 sims)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STEP_BYTES = 43            # algorithmic bytes per board step
+MFMA16_PEAK = 2500.0       # dense bf16 / fp16 MFMA TFLOP/s (MI355X_MICROARCH.md)
+MFMA32_PEAK = 157.3        # dense fp32 MFMA TFLOP/s
+DTYPE_LABEL = {
+    "split3": "fp32-accurate net (trunk: fp32 operands split into 3 bf16 words, 6 bf16 MFMA "
+              "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
+    "fp32": "fp32 (net), int64 bitboards",
+    "fp16": "fp16 trunk operands, fp32 accumulation (net), int64 bitboards",
+}
 
 
 def parse():
@@ -64,6 +75,10 @@ def parse():
     ap.add_argument("--games", type=int, default=None, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--net", default=None, choices=["az5x128", "fast"])
+    ap.add_argument("--conv-precision", default=None, choices=["split3", "fp32", "fp16"],
+                    help="3x3 trunk arithmetic: split3 = bf16x3-split operands on the 16-bit "
+                         "MFMA pipe, fp32 accumulation, fp32-accurate (default for c2/c3); "
+                         "fp32 = fp32 MFMA; fp16 = fp16 operands (c5's fp16 inference)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="simulation steps captured per HIP graph (1 under rocprofv3: its "
@@ -80,6 +95,7 @@ def parse():
     a.sims = a.sims or preset[1]
     a.net = a.net or preset[2]
     a.d4, a.precision = preset[3], preset[4]
+    a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "split3")
     return a
 
 
@@ -135,10 +151,12 @@ def kernel_roofline(positions, n, device):
 
 
 def conv_roofline(sp, device, n_boards):
-    """The step's dominant kernel (k_conv3x3: ~90 % of a step's GPU time) timed with HIP
-    events on its launch stream, at the bench's leaf batch, with the net's own weights:
-    achieved = 2*B*64*C*C*9 FLOP per launch / average launch time, against the dense fp32
-    MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md)."""
+    """The step's dominant kernel (the fused 3x3 trunk conv: ~90 % of a step's GPU time)
+    timed with HIP events on its launch stream, at the bench's leaf batch, with the net's
+    own weights.  achieved = MFMA FLOP executed per launch / average launch time against
+    the dense peak of the pipe it runs on: split3 executes 6 bf16 products per fp32
+    multiply-add (2*B*64*C*C*9 algorithmic FLOP x 6) against 2.5 PFLOP/s; fp16 1x against
+    2.5 PFLOP/s; fp32 1x against 157.3 TFLOP/s (MI355X_MICROARCH.md)."""
     import az_native as nat
 
     conv = sp.net.c2[0]
@@ -146,25 +164,36 @@ def conv_roofline(sp, device, n_boards):
     x = torch.randn(n_boards, C, 8, 8, device=device).contiguous(memory_format=torch.channels_last)
     r = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
     y = torch.empty_like(x)
-    args = [nat.ptr(x), nat.ptr(conv.w9), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y), n_boards, C,
-            1, nat.stream_ptr()]
+    if conv.precision == "fp32":
+        fn = nat.lib.az_conv3x3_gpu
+        args = [nat.ptr(x), nat.ptr(conv.w9), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y),
+                n_boards, C, 1, nat.stream_ptr()]
+        kname, mult, peak = "k_conv3x3 (az_conv3x3_gpu, fp32 MFMA)", 1, MFMA32_PEAK
+    else:
+        fn = nat.lib.az_conv3x3_mx_gpu
+        args = [nat.ptr(x), nat.ptr(conv.wq), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y),
+                n_boards, C, 1, conv.mode, nat.stream_ptr()]
+        mult = 6 if conv.precision == "split3" else 1
+        kname, peak = f"k_conv3x3_mx (az_conv3x3_mx_gpu, {conv.precision})", MFMA16_PEAK
     for _ in range(3):
-        nat.check(nat.lib.az_conv3x3_gpu(*args), "az_conv3x3_gpu")
+        nat.check(fn(*args), kname)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 50
     ev0.record()
     for _ in range(reps):
-        nat.lib.az_conv3x3_gpu(*args)
+        fn(*args)
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / reps
     flop = 2.0 * n_boards * 64 * C * C * 9
-    achieved = flop / (ms * 1e-3) / 1e12
-    return {"kernel": "k_conv3x3 (az_conv3x3_gpu, fused bias+residual+ReLU)", "bound": "mfma",
-            "achieved": round(achieved, 1), "peak": 157.3, "unit": "TFLOP/s",
-            "frac": round(achieved / 157.3, 4), "traffic": None, "boards": n_boards,
-            "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop}
+    achieved = mult * flop / (ms * 1e-3) / 1e12
+    return {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
+            "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "boards": n_boards,
+            "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+            "mfma_flop_per_algorithmic_flop": mult,
+            "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1)}
 
 
 def cpu_baseline(net, seconds):
@@ -241,7 +270,8 @@ def main():
     sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
                          use_graph=not a.no_graph, device=device, d4_augment=a.d4,
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
-                         sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph)
+                         sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
+                         precision=a.conv_precision)
     e = sp.engine
     # stagger slot starts over the warmup (at least one move length) so moves complete at a
     # steady rate in the window
@@ -301,7 +331,7 @@ def main():
         "value": round(float(value), 4), "unit": "games/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(t_max * 1000.0 / a.steps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": f"{a.precision} (net), int64 bitboards",
+        "scaling": "weak", "vs_baseline": None, "dtype": DTYPE_LABEL[a.conv_precision],
         "data": "synthetic: self-play from the initial position, random-init net weights",
         "config": {"workload": {"c3": "configs[2]: 8x8 Othello, 400 sims/move, AlphaZeroNet(5x128) "
                                       "random init fp32, leaf batch 1024 = concurrent games",

@@ -67,8 +67,8 @@ def test_bias_act_kernel_matches_torch():
 
 
 @pytest.mark.parametrize("kind", ["az", "fast"])
-@pytest.mark.parametrize("conv", ["hip", "miopen"])
-def test_inference_copy_matches_module(kind, conv):
+@pytest.mark.parametrize("conv,precision", [("hip", "split3"), ("hip", "fp32"), ("miopen", None)])
+def test_inference_copy_matches_module(kind, conv, precision):
     torch.manual_seed(0)
     net = AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)
     # non-trivial BatchNorm statistics so the folding is exercised
@@ -79,7 +79,7 @@ def test_inference_copy_matches_module(kind, conv):
             m.weight.data.uniform_(0.5, 1.5)
             m.bias.data.uniform_(-0.2, 0.2)
     net = net.cuda().eval()
-    fused = inference_copy(net, "cuda", conv=conv)
+    fused = inference_copy(net, "cuda", conv=conv, precision=precision)
     x = torch.randint(-1, 2, (257, 64), device="cuda").float()
     with torch.no_grad():
         logits, v = net(x.view(-1, 1, 8, 8))
@@ -149,3 +149,19 @@ def test_conv3x3_fp16_mode(C, res):
     y = _mx_conv(x, w, b, r if res else None, True, nat.AZ_CONV_FP16)
     ref = F.relu(ref64 + (r.cpu().double() if res else 0)).float().cuda()
     torch.testing.assert_close(y, ref, atol=5e-3, rtol=5e-3)
+
+
+@pytest.mark.parametrize("kind", ["az", "fast"])
+def test_inference_copy_fp16_trunk(kind):
+    """config #5: fp16 trunk operands (fp32 accumulation, fp32 activations/heads) stay
+    within fp16 rounding of the fp32 module."""
+    torch.manual_seed(1)
+    net = (AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)).cuda().eval()
+    fused = inference_copy(net, "cuda", dtype=torch.float16)
+    assert fused.precision == "fp16"
+    x = torch.randint(-1, 2, (129, 64), device="cuda").float()
+    with torch.no_grad():
+        logits, v = net(x.view(-1, 1, 8, 8))
+        p, val = fused.evaluate_planes(x)
+    torch.testing.assert_close(p, torch.softmax(logits, -1), atol=2e-3, rtol=2e-2)
+    torch.testing.assert_close(val, v.reshape(-1), atol=2e-3, rtol=2e-2)
