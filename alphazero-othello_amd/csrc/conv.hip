@@ -52,12 +52,21 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
   // all-zero position (index kBoards*64) is what off-board taps read (branch-free gather)
   {
     constexpr int V = (kBoards * 64 + 1) * C / 4;  // float4s
+    constexpr int ITER = (V + kThreads - 1) / kThreads;
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
-    for (int v = tid; v < V; v += kThreads) {
+    float4 val[ITER];  // every load issued before the first LDS write
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      val[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (v < nb * 64 * (C / 4)) val[i] = src[v];
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      if (v >= V) continue;
       const int pos = v / (C / 4), c4 = v % (C / 4);
-      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (pos < nb * 64) val = src[v];
-      *reinterpret_cast<float4*>(lds + pos * G::S + c4 * 4) = val;
+      *reinterpret_cast<float4*>(lds + pos * G::S + c4 * 4) = val[i];
     }
   }
   __syncthreads();

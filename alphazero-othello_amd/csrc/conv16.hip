@@ -169,14 +169,25 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   // split of every activation done once here, not once per tap); zero-fill a missing tail
   // board and the all-zero position (index kBoards*64) that off-board taps read
   {
+    // every load issued before the first conversion (one HBM round trip, not one per
+    // iteration)
     constexpr int V = (kBoards * 64 + 1) * C / 4;
+    constexpr int ITER = (V + kThreads - 1) / kThreads;
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
-    for (int v = tid; v < ((AZ_MX_EXP & 4) ? 0 : V); v += kThreads) {
+    float4 val[ITER];
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      val[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(AZ_MX_EXP & 4) && v < nb * 64 * (C / 4)) val[i] = src[v];
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      if ((AZ_MX_EXP & 4) || v >= V) continue;
       const int pos = v / (C / 4), c4 = v % (C / 4);
-      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (pos < nb * 64) val = src[v];
       char* dst = lds_a + pos * G::APOS + c4 * 8;
-      const f32x4 a = {val.x, val.y, val.z, val.w};
+      const f32x4 a = {val[i].x, val[i].y, val[i].z, val[i].w};
       if constexpr (G::MODE == AZ_CONV_SPLIT3) {
         const bf16x4 x0 = __builtin_convertvector(a, bf16x4);
         const f32x4 r1 = a - __builtin_convertvector(x0, f32x4);
@@ -247,19 +258,25 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   // 32-row tile lies inside one board, so the tail-board test is uniform per tile
   const int co = col0 + r;
   const float bv = bias[co];
+  float rv[G::TM][16];
+  if (RES) {  // all residual loads in flight at once
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi) {
+      const size_t o0 = ((size_t)b0 * 64 + 32 * mi + 4 * h) * C + co;
+      const bool in = ((32 * mi) >> 6) < nb;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        rv[mi][k] = in ? res[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C] : 0.0f;
+    }
+  }
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi) {
     if (((32 * mi) >> 6) >= nb) continue;
     const size_t o0 = ((size_t)b0 * 64 + 32 * mi + 4 * h) * C + co;
-    float rv[16];
-    if (RES) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) rv[k] = res[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C];
-    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       float v = acc[mi][k] + bv;
-      if (RES) v += rv[k];
+      if (RES) v += rv[mi][k];
       if (RELU) v = fmaxf(v, 0.0f);
       if (AZ_MX_EXP & 8) {
         if (v == 12345.f) y[o0] = v;
