@@ -335,13 +335,65 @@ class FusedInferenceNet(nn.Module, Inference):
         self.c1 = nn.ModuleList([C3(b.conv1) for b in blocks])
         self.c2 = nn.ModuleList([C3(b.conv2) for b in blocks])
 
-    def forward(self, x):
+    def _trunk(self, x):
         if x.dim() == 3:
             x = x.unsqueeze(1)
         x = x.contiguous(memory_format=torch.channels_last)
         h = self.stem(x)
         for c1, c2 in zip(self.c1, self.c2):
             h = c2(c1(h), res=h)
+        return h
+
+    def _fused_heads_ready(self):
+        if self.kind != "az" or self.conv_impl != "hip":
+            return False
+        if not hasattr(self, "_hw"):
+            C = self.heads.weight.shape[1]
+            pol, v1, v2 = self.pol_fc, self.val_fc1, self.val_fc2
+            self._hw = {
+                "wpv": self.heads.weight.detach().reshape(3, C).float().contiguous(),
+                "bpv": self.heads.bias.detach().float().contiguous(),
+                "wpolT": pol.weight.detach().float().t().contiguous(),      # [128][65]
+                "bpol": pol.bias.detach().float().contiguous(),
+                "w1T": v1.weight.detach().float().t().contiguous(),         # [64][256]
+                "b1": v1.bias.detach().float().contiguous(),
+                "w2": v2.weight.detach().float().reshape(-1).contiguous(),  # [256]
+                "b2": v2.bias.detach().float().contiguous(),
+                "C": C,
+            }
+        return True
+
+    def evaluate_into(self, planes, priors, values):
+        """Leaf evaluation straight into the engine's buffers: priors float32 [B, 65]
+        (softmax), values float32 [B] (tanh).  AlphaZeroNet on the HIP trunk runs both heads
+        in one kernel (csrc/heads.hip); otherwise the module's heads + copies."""
+        if not self._fused_heads_ready():
+            p, v = self.evaluate_planes(planes)
+            priors.copy_(p)
+            values.copy_(v)
+            return
+        import az_native as nat
+
+        B = planes.shape[0]
+        h = self._trunk(planes.view(B, 1, 8, 8))
+        hw = self._hw
+        nat.check(nat.lib.az_heads_az_gpu(
+            nat.ptr(h), nat.ptr(hw["wpv"]), nat.ptr(hw["bpv"]), nat.ptr(hw["wpolT"]),
+            nat.ptr(hw["bpol"]), nat.ptr(hw["w1T"]), nat.ptr(hw["b1"]), nat.ptr(hw["w2"]),
+            nat.ptr(hw["b2"]), nat.ptr(priors), nat.ptr(values), B, hw["C"], nat.stream_ptr()),
+            "az_heads_az_gpu")
+
+    def evaluate_planes(self, planes):
+        if not self._fused_heads_ready():
+            return Inference.evaluate_planes(self, planes)
+        B = planes.shape[0]
+        pr = torch.empty(B, 65, dtype=torch.float32, device=planes.device)
+        va = torch.empty(B, dtype=torch.float32, device=planes.device)
+        self.evaluate_into(planes.float(), pr, va)
+        return pr, va
+
+    def forward(self, x):
+        h = self._trunk(x)
         B = h.shape[0]
         if self.kind == "az":
             y = self.heads(h)

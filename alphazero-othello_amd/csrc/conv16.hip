@@ -57,7 +57,7 @@ struct Mx {
   static constexpr int CHUNKS = C / 16, STEPS = 9 * CHUNKS;
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes per (tap, chunk) step
   static constexpr size_t LDS_BYTES = A_BYTES;
-  static_assert(STEPS % 6 == 0, "the main loop is unrolled by 6");
+  static_assert(CHUNKS % 4 == 0, "the chunk loop is unrolled by 4");
 };
 
 template <class G>
@@ -72,35 +72,39 @@ struct BFrag {
   Word8<G> v[G::PLANES];
 };
 
-// A fragments of step s: lane (r, h) of tile mi reads, per plane, the 8 words of channels
-// ci0+8h.. of its row's tapped position (or of the all-zero position)
+// LDS byte offset of the A row each tile's lane reads at `tap` (its tapped position, or
+// the all-zero position), with the lane's k-half folded in
 template <class G>
-__device__ __forceinline__ void mx_read_a(AFrag<G>& f, const char* lds_a, int s,
-                                          const int (&pos0)[G::TM], const int (&ok9)[G::TM],
-                                          int h) {
-  const int tap = s / G::CHUNKS, ci0 = (s % G::CHUNKS) * 16;
+__device__ __forceinline__ void mx_tap_base(int (&base)[G::TM], int tap,
+                                            const int (&pos0)[G::TM], const int (&ok9)[G::TM],
+                                            int h) {
   const int d = (tap / 3 - 1) * 8 + (tap % 3 - 1);
-  const char* p[G::TM];
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi) {
     const int pos = (ok9[mi] >> tap) & 1 ? pos0[mi] + d : G::BOARDS * 64;
-    p[mi] = lds_a + pos * G::APOS + (ci0 + 8 * h) * 2;
+    base[mi] = pos * G::APOS + 16 * h;
   }
-  // issued in the order mx_mma consumes them: the last plane (x2) first
+}
+
+// A fragments of (tap, chunk ch): per plane, the 8 words of channels 16ch+8h.. (the chunk
+// and plane offsets are ds_read immediates); issued in the order mx_mma consumes them
+template <class G>
+__device__ __forceinline__ void mx_read_a(AFrag<G>& f, const char* lds_a,
+                                          const int (&base)[G::TM], int ch) {
 #pragma unroll
   for (int pl = G::PLANES - 1; pl >= 0; --pl)
 #pragma unroll
     for (int mi = 0; mi < G::TM; ++mi)
-      f.v[pl][mi] = *reinterpret_cast<const Word8<G>*>(p[mi] + pl * G::C * 2);
+      f.v[pl][mi] = *reinterpret_cast<const Word8<G>*>(lds_a + base[mi] + ch * 32 + pl * G::C * 2);
 }
 
 // B fragments of step s: this lane's 16 bytes of each plane (column col0 + r, k = 8h..)
 template <class G>
-__device__ __forceinline__ void mx_load_b(BFrag<G>& f, const char* wlane, int s) {
+__device__ __forceinline__ void mx_load_b(BFrag<G>& f, const char* wq, int lane_off, int s) {
+  const char* step = wq + (size_t)s * G::STEP_BYTES;  // uniform base: saddr + lane offset
 #pragma unroll
   for (int pl = 0; pl < G::PLANES; ++pl)
-    f.v[pl] = *reinterpret_cast<const Word8<G>*>(wlane + (size_t)s * G::STEP_BYTES +
-                                                 pl * G::C * 32);
+    f.v[pl] = *reinterpret_cast<const Word8<G>*>(step + lane_off + pl * G::C * 32);
 }
 
 template <class G>
@@ -128,7 +132,6 @@ template <class G>
 __device__ __forceinline__ void mx_sched() {
   constexpr int kMfma = (G::MODE == AZ_CONV_SPLIT3 ? 6 : 1) * G::TM;
   constexpr int kDs = G::PLANES * G::TM;
-  __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);  // VALU (addresses)
   constexpr int kPer = kMfma / kDs > 0 ? kMfma / kDs : 1;
 #pragma unroll
   for (int i = 0; i < kDs; ++i) {
@@ -159,11 +162,11 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   constexpr int last = G::STEPS - 1;
 
   // weights of the first three steps are in flight while the boards are staged
-  const char* wlane = wq + (size_t)(col0 + r) * 32 + h * 16;
-  BFrag<G> b0f, b1f, b2f;
-  mx_load_b<G>(b0f, wlane, 0);
-  mx_load_b<G>(b1f, wlane, 1);
-  mx_load_b<G>(b2f, wlane, 2);
+  const int wlane = (col0 + r) * 32 + h * 16;
+  BFrag<G> b0f, b1f, b2f, b3f;
+  mx_load_b<G>(b0f, wq, wlane, 0);
+  mx_load_b<G>(b1f, wq, wlane, 1);
+  mx_load_b<G>(b2f, wq, wlane, 2);
 
   // ---- stage the input boards (NHWC) into LDS as PLANES 16-bit words per element (the
   // split of every activation done once here, not once per tap); zero-fill a missing tail
@@ -225,32 +228,42 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[mi][k] = 0.0f;
 
-  // Step s: MFMAs on A set s%2 and B set s%3; then B set s%3 is reloaded with step s+3 and
-  // A set (s+1)%2 read for step s+1.  Indices are clamped to the last step so every load
-  // is unconditional (exact vmcnt bookkeeping); the surplus loads are never consumed.
-  AFrag<G> a0f, a1f;
-  mx_read_a<G>(a0f, lds_a, 0, pos0, ok9, h);
+  // Step s = (tap, chunk): MFMAs on A set s%2 and B set s%4; the A set of step s+1 is read
+  // meanwhile (next tap's row offsets precomputed at the tap's start) and B set (s+3)%4 —
+  // consumed by step s-1 — reloaded with step s+3.  Indices are clamped to the last step
+  // so every load is unconditional (exact vmcnt bookkeeping); surplus loads are unused.
   // The machine scheduler would put a step's loads in one burst ahead of its MFMAs (the
-  // MFMA pipe then idles while they issue) or sink them behind; sched_group_barrier pins
-  // the issue pattern: address VALU first, then each LDS read of the next step's A in the
-  // shadow of two MFMAs, then the weight loads behind the MFMAs that consume their
-  // registers.
-#define AZ_MX_STEP(S, AC, AN, BC)                                                 \
-  {                                                                               \
-    const int s_ = (S);                                                           \
-    if (!(AZ_MX_EXP & 1))                                                         \
-      mx_read_a<G>(AN, lds_a, s_ + 1 < last ? s_ + 1 : last, pos0, ok9, h);       \
-    mx_mma<G>(acc, AC, BC);                                                       \
-    if (!(AZ_MX_EXP & 2)) mx_load_b<G>(BC, wlane, s_ + 3 < last ? s_ + 3 : last); \
-    mx_sched<G>();                                                                \
+  // MFMA pipe then idles while they issue) or sink them behind; mx_sched pins the issue
+  // pattern: each LDS read in the shadow of two MFMAs, the weight loads behind the MFMAs.
+  static_assert(G::CHUNKS % 4 == 0, "B ring of 4 and A ring of 2 within a tap");
+  AFrag<G> a0f, a1f;
+  int bcur[G::TM], bnxt[G::TM];
+  mx_tap_base<G>(bcur, 0, pos0, ok9, h);
+  mx_read_a<G>(a0f, lds_a, bcur, 0);
+#define AZ_MX_STEP(CH, AC, AN, BC, BL)                                              \
+  {                                                                                 \
+    const int s_ = tap * G::CHUNKS + (CH);                                          \
+    if (!(AZ_MX_EXP & 1)) {                                                         \
+      if ((CH) + 1 < G::CHUNKS)                                                     \
+        mx_read_a<G>(AN, lds_a, bcur, (CH) + 1);                                    \
+      else                                                                          \
+        mx_read_a<G>(AN, lds_a, bnxt, 0);                                           \
+    }                                                                               \
+    mx_mma<G>(acc, AC, BC);                                                         \
+    if (!(AZ_MX_EXP & 2)) mx_load_b<G>(BL, wq, wlane, s_ + 3 < last ? s_ + 3 : last); \
+    mx_sched<G>();                                                                  \
   }
-  for (int s = 0; s < G::STEPS; s += 6) {
-    AZ_MX_STEP(s + 0, a0f, a1f, b0f)
-    AZ_MX_STEP(s + 1, a1f, a0f, b1f)
-    AZ_MX_STEP(s + 2, a0f, a1f, b2f)
-    AZ_MX_STEP(s + 3, a1f, a0f, b0f)
-    AZ_MX_STEP(s + 4, a0f, a1f, b1f)
-    AZ_MX_STEP(s + 5, a1f, a0f, b2f)
+  for (int tap = 0; tap < 9; ++tap) {
+    mx_tap_base<G>(bnxt, tap + 1 < 9 ? tap + 1 : 8, pos0, ok9, h);
+#pragma unroll
+    for (int c4 = 0; c4 < G::CHUNKS; c4 += 4) {
+      AZ_MX_STEP(c4 + 0, a0f, a1f, b0f, b3f)
+      AZ_MX_STEP(c4 + 1, a1f, a0f, b1f, b0f)
+      AZ_MX_STEP(c4 + 2, a0f, a1f, b2f, b1f)
+      AZ_MX_STEP(c4 + 3, a1f, a0f, b3f, b2f)
+    }
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi) bcur[mi] = bnxt[mi];
   }
 #undef AZ_MX_STEP
 

@@ -282,9 +282,12 @@ class BatchedSelfPlay:
         e = self.engine
         e.select()
         if self.net is not None:
-            pr, va = self.net.evaluate_planes(e.nn_in)
-            e.priors.copy_(pr)
-            e.values.copy_(va)
+            if hasattr(self.net, "evaluate_into"):
+                self.net.evaluate_into(e.nn_in, e.priors, e.values)
+            else:
+                pr, va = self.net.evaluate_planes(e.nn_in)
+                e.priors.copy_(pr)
+                e.values.copy_(va)
         e.expand()
         e.play()
 

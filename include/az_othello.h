@@ -283,6 +283,17 @@ int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias, const f
                       float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t mode,
                       void* stream);
 
+/* AlphaZeroNet's policy and value heads in one kernel (reference Models.py:196-221 with
+ * BatchNorm folded, softmax of MCTS_model.py:319): h NHWC float [n_boards, 8, 8, C];
+ * wpv [3][C] (rows: policy ch 0, policy ch 1, value) and bpv [3] the 1x1 convs; wpolT
+ * [128][65] = pol_fc.weight^T, bpol [65]; w1T [64][256] = val_fc1.weight^T, b1 [256];
+ * w2 [256], b2 [1] = val_fc2.  Writes priors [n_boards][65] (softmax) and values
+ * [n_boards] (tanh).  16-byte aligned h / wpv / w1T / b1 / w2. */
+int az_heads_az_gpu(const float* h, const float* wpv, const float* bpv, const float* wpolT,
+                    const float* bpol, const float* w1T, const float* b1, const float* w2,
+                    const float* b2, float* priors, float* values, int32_t n_boards,
+                    int32_t channels, void* stream);
+
 /* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
  * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,
  * 186-187). */
