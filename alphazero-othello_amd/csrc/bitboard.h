@@ -352,6 +352,24 @@ AZ_HD Move move_rays(const uint64_t* rays, uint64_t own, uint64_t opp, int act) 
   return m;
 }
 
+// move_rays() without branches (the batched kernel's form: a wave never diverges on the
+// pass / illegal cases, which cost four selects instead).
+AZ_HD Move move_rays_bf(const uint64_t* rays, uint64_t own, uint64_t opp, int act) {
+  const int sq = act & 63;
+  const uint64_t nb = 1ull << sq;
+  const uint64_t cap =
+      flips_rays(rays + 4 * sq, rays + 4 * (63 - sq), own, opp, rev64(own), rev64(opp));
+  const bool place = (unsigned)act < 64u && cap != 0ull && !(nb & (own | opp));
+  const bool pass = act == kPass;
+  const uint64_t c = place ? cap : 0ull, b = place ? nb : 0ull;
+  Move m;
+  m.illegal = !(place || pass);
+  m.flags = pass ? kFlagPassed : 0;
+  m.own = m.illegal ? own : opp ^ c;
+  m.opp = m.illegal ? opp : bop3<tt::A ^ tt::B ^ tt::C>(own, b, c);
+  return m;
+}
+
 // One board step for one position: placement or pass, then the next side's legal mask,
 // terminal check and disc difference.  Illegal placements leave the board unchanged and
 // set kFlagIllegal (the reference raises ValueError at envs/othello.py:419-421).
@@ -374,7 +392,7 @@ AZ_HD Step step(uint64_t own, uint64_t opp, int act) {
 // step() on the ray-table capture set (the batched entry points' formulation).
 AZ_HD Step step_rays(const uint64_t* rays, uint64_t own, uint64_t opp, int act) {
   Step o;
-  const Move m = move_rays(rays, own, opp, act);
+  const Move m = move_rays_bf(rays, own, opp, act);
   o.own = m.own;
   o.opp = m.opp;
   if (m.illegal) {

@@ -36,8 +36,10 @@ static_assert(kBlock == 64 * 4, "k_step stages one up-ray per thread");
 
 // One position per lane per iteration, grid-stride.  Every global access is a
 // lane-contiguous 8-byte (own/opp/legal), 1-byte (act) or 2-byte (status) access, so a
-// wave moves 64 consecutive positions per instruction.  The capture set comes from the
-// 2 KB up-ray table staged once per workgroup in LDS (two ds_read_b128 per ray set).
+// wave moves 64 consecutive positions per instruction; 32-bit byte offsets off the
+// uniform array bases (n < 2^28: the host checks) keep address math off the 64-bit VALU.
+// The capture set comes from the 2 KB up-ray table staged once per workgroup in LDS (two
+// ds_read_b128 per ray set); the make-move is branch-free (move_rays_bf).
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ own,
                                                  const uint64_t* __restrict__ opp,
                                                  const uint8_t* __restrict__ act,
@@ -45,31 +47,34 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
                                                  uint64_t* __restrict__ opp_o,
                                                  uint64_t* __restrict__ legal_o,
                                                  uint16_t* __restrict__ status_o,
-                                                 int64_t n) {
+                                                 uint32_t n) {
   __shared__ __align__(16) uint64_t rays[64 * 4];
   rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
   __syncthreads();
   // every lane runs the same number of iterations (the terminal check is wave-cooperative)
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  const int64_t n_pad = (n + kBlock - 1) / kBlock * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t n_pad = (n + kBlock - 1) / kBlock * kBlock;
+  const char* own_b = reinterpret_cast<const char*>(own);
+  const char* opp_b = reinterpret_cast<const char*>(opp);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
     const bool live = i < n;
+    const uint32_t o8 = i * 8u;
     uint64_t o = 0, p = 0;
     int a = azb::kPass;
     if (live) {
-      o = own[i];
-      p = opp[i];
+      o = *reinterpret_cast<const uint64_t*>(own_b + o8);
+      p = *reinterpret_cast<const uint64_t*>(opp_b + o8);
       a = act[i];
     }
-    const azb::Move mv = azb::move_rays(rays, o, p, a);
+    const azb::Move mv = azb::move_rays_bf(rays, o, p, a);
     const bool ok = live && !mv.illegal;
     const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
     int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
     tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
     if (live) {
-      own_o[i] = mv.own;
-      opp_o[i] = mv.opp;
-      legal_o[i] = lg;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(own_o) + o8) = mv.own;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(opp_o) + o8) = mv.opp;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(legal_o) + o8) = lg;
       status_o[i] = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0)
                                : azb::pack_status(mv.flags | tf,
                                                   azb::popc(mv.own) - azb::popc(mv.opp));
@@ -227,8 +232,10 @@ int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   if (n == 0) return AZ_OK;
   AZ_REQUIRE(own && opp && act && own_o && opp_o && legal_o && status_o, AZ_ERR_ARG,
              "oth_step_gpu: null buffer");
+  AZ_REQUIRE(n < (int64_t(1) << 28), AZ_ERR_ARG,
+             "oth_step_gpu: n=%lld exceeds 2^28 positions per call", (long long)n);
   hipLaunchKernelGGL(k_step, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
-                     own, opp, act, own_o, opp_o, legal_o, status_o, n);
+                     own, opp, act, own_o, opp_o, legal_o, status_o, (uint32_t)n);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -34,11 +34,14 @@ for v in VARS:
         e1.record(); torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 20
         ok = None
-        if v in (0, 2, 3, 7, 9, 11, 13, 14, 16, 17, 18, 21, 22, 23, 24, 25, 26):
+        if v in (0, 2, 3, 7, 9, 11, 13, 14, 16, 17, 18, 21, 22, 23, 24, 25, 26, 32, 33, 34):
             outs = [o.cpu() for o in O]
             if ref is None: ref = outs
             ok = all(bool((a == b).all()) for a, b in zip(outs, ref))
         if v in (5, 6):
             ok = bool((O[2].cpu() == ref[2]).all()) if False else None
         res[f"v{v}_g{grid}"] = {"ms": round(ms, 4), "gsteps": round(n / ms / 1e6, 1), "alg_TBps": round(43 * n / ms / 1e9, 3), "ok": ok}
+        if v in (29, 30, 31):
+            st = O[2][n - 4:].cpu().numpy()
+            res[f"v{v}_g{grid}"]["clock_GHz"] = round(float(st[1] - st[0]) / float(st[3] - st[2]) * 0.1, 3)
 print(json.dumps(res, indent=0))

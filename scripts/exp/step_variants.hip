@@ -437,11 +437,109 @@ __global__ __launch_bounds__(256) void v28(const uint64_t* own, const uint64_t* 
     __builtin_nontemporal_store(a | b, lo + i); __builtin_nontemporal_store((uint16_t)c, so + i); }
 }
 
+// v29 / v30: v17 / v19 with clock stamps (block 0, lane 0): s_memtime (shader clock) and
+// s_memrealtime (100 MHz) at start and end, written to oo[n-4 .. n-1] after the work
+__global__ __launch_bounds__(256) void v29(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  RAYS
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n - 4; i += (int64_t)gridDim.x * 256) {
+    azb::Step s = azb::step_rays(rays, own[i], opp[i], act[i]); oo[i] = s.own; po[i] = s.opp; lo[i] = s.legal; so[i] = s.status; }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x == 0) { lo[n - 4] = t0; lo[n - 3] = t1; lo[n - 2] = r0; lo[n - 1] = r1; }
+}
+__global__ __launch_bounds__(256) void v30(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  RAYS
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t base_o = own[t & 32767], base_p = opp[t & 32767];
+  const int base_a = act[t & 32767];
+  uint64_t acc = 0;
+  for (int64_t i = t; i < n; i += (int64_t)gridDim.x * 256) {
+    azb::Step s = azb::step_rays(rays, base_o ^ acc, base_p, (base_a + (int)(i >> 20)) & 63);
+    acc ^= (s.own ^ s.opp ^ s.legal ^ s.status) & 1;
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (t < n - 4) lo[t] = acc;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { lo[n - 4] = t0; lo[n - 3] = t1; lo[n - 2] = r0; lo[n - 1] = r1; }
+}
+// v31: I/O only (v1) with stamps
+__global__ __launch_bounds__(256) void v31(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n - 4; i += (int64_t)gridDim.x * 256) {
+    uint64_t a = own[i], b = opp[i]; int c = act[i]; oo[i] = a ^ c; po[i] = b; lo[i] = a | b; so[i] = (uint16_t)c; }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x == 0) { lo[n - 4] = t0; lo[n - 3] = t1; lo[n - 2] = r0; lo[n - 1] = r1; }
+}
+
+// v32: the product k_step body (cooperative terminal check) — A/B reference for v33/v34
+__global__ __launch_bounds__(256) void v32(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t n_pad = (n + 255) / 256 * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    uint64_t o = 0, p = 0; int a = azb::kPass;
+    if (live) { o = own[i]; p = opp[i]; a = act[i]; }
+    const azb::Move mv = azb::move_rays(rays, o, p, a);
+    const bool ok = live && !mv.illegal;
+    const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+    int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+    tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+    if (live) {
+      oo[i] = mv.own; po[i] = mv.opp; lo[i] = lg;
+      so[i] = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(mv.flags | tf, azb::popc(mv.own) - azb::popc(mv.opp));
+    }
+  }
+}
+// v33: branch-free move + 32-bit byte offsets (saddr loads/stores)
+template <bool BF>
+__device__ __forceinline__ void step33(const uint64_t* rays, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, uint32_t n) {
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t n_pad = (n + 255) / 256 * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    const uint32_t o8 = i * 8u;
+    uint64_t o = 0, p = 0; int a = azb::kPass;
+    if (live) {
+      o = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(own) + o8);
+      p = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(opp) + o8);
+      a = act[i];
+    }
+    const azb::Move mv = BF ? azb::move_rays_bf(rays, o, p, a) : azb::move_rays(rays, o, p, a);
+    const bool ok = live && !mv.illegal;
+    const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+    int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+    tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+    if (live) {
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(oo) + o8) = mv.own;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(po) + o8) = mv.opp;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lo) + o8) = lg;
+      *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(so) + i * 2u) = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(mv.flags | tf, azb::popc(mv.own) - azb::popc(mv.opp));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void v33(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  step33<true>(rays, own, opp, act, oo, po, lo, so, (uint32_t)n);
+}
+// v34: 32-bit offsets only
+__global__ __launch_bounds__(256) void v34(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  step33<false>(rays, own, opp, act, oo, po, lo, so, (uint32_t)n);
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28};
-  if (v < 0 || v > 28) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34};
+  if (v < 0 || v > 34) return -1;
   const int blk = v == 14 ? 64 : 256;
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
