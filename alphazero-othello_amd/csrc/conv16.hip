@@ -13,9 +13,11 @@
 //     MFMAs cost 6/16 of one fp32 MFMA of the same shape.
 //   AZ_CONV_FP16: one fp16 product (BASELINE configs[4]'s fp16 inference).
 //
-// GEMM view: M = B*64 output positions, N = C, K = 9 taps x C.  Workgroup = 2 boards
-// (M = 128 rows) x all C columns; wave w owns all 128 rows x columns 32w..32w+31 (4 x 1
-// tiles of 32x32), so each weight fragment feeds four MFMAs.
+// GEMM view: M = B*64 output positions, N = C, K = 9 taps x C.  Workgroup = 1 board
+// (M = 64 rows; 51 KB of LDS: 3 workgroups per CU, so one workgroup's staging and
+// epilogue overlap another's MFMAs) or 2 boards (cfg 0: 101 KB, one per CU) x all C
+// columns; wave w owns all the rows x columns 32w..32w+31, so each weight fragment feeds
+// two (four) MFMAs.
 //   * A: the two boards are split into PLANES 16-bit words per element ONCE, while being
 //     staged into LDS as [position][plane][C] (+16 B per position: conflict-free
 //     ds_read_b128 row gathers; one all-zero position for the off-board taps), and stay
@@ -45,12 +47,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
-template <int C_, int MODE_>
+template <int C_, int MODE_, int BOARDS_ = 2>
 struct Mx {
   static constexpr int C = C_, MODE = MODE_;
   static constexpr int PLANES = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
-  static constexpr int BOARDS = 2;
-  static constexpr int TM = 4;                      // 32-row tiles per wave (= 128 rows)
+  static constexpr int BOARDS = BOARDS_;
+  static constexpr int TM = 2 * BOARDS;             // 32-row tiles per wave (= all rows)
   static constexpr int WAVES = C / 32, THREADS = 64 * WAVES;
   static constexpr int APOS = PLANES * C * 2 + 16;  // LDS bytes per staged position
   static constexpr int A_BYTES = (BOARDS * 64 + 1) * APOS;
@@ -374,24 +376,47 @@ extern "C" int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channel
   return AZ_OK;
 }
 
+namespace {
+int launch_mx_cfg(const float* x, const void* wq, const float* bias, const float* res, float* y,
+                  int n_boards, int channels, int relu, int mode, int cfg, hipStream_t s) {
+  // cfg 0: 2 boards per workgroup (each weight fragment feeds 4 MFMAs); cfg 1: 1 board
+  // (half the LDS, 2-3 workgroups per CU, 2 MFMAs per weight fragment)
+  const bool two = cfg == 0;
+  if (channels == 128 && mode == AZ_CONV_SPLIT3)
+    return two ? launch_mx<Mx<128, AZ_CONV_SPLIT3, 2>>(x, wq, bias, res, y, n_boards, relu, s)
+               : launch_mx<Mx<128, AZ_CONV_SPLIT3, 1>>(x, wq, bias, res, y, n_boards, relu, s);
+  if (channels == 64 && mode == AZ_CONV_SPLIT3)
+    return two ? launch_mx<Mx<64, AZ_CONV_SPLIT3, 2>>(x, wq, bias, res, y, n_boards, relu, s)
+               : launch_mx<Mx<64, AZ_CONV_SPLIT3, 1>>(x, wq, bias, res, y, n_boards, relu, s);
+  if (channels == 128 && mode == AZ_CONV_FP16)
+    return two ? launch_mx<Mx<128, AZ_CONV_FP16, 2>>(x, wq, bias, res, y, n_boards, relu, s)
+               : launch_mx<Mx<128, AZ_CONV_FP16, 1>>(x, wq, bias, res, y, n_boards, relu, s);
+  if (channels == 64 && mode == AZ_CONV_FP16)
+    return two ? launch_mx<Mx<64, AZ_CONV_FP16, 2>>(x, wq, bias, res, y, n_boards, relu, s)
+               : launch_mx<Mx<64, AZ_CONV_FP16, 1>>(x, wq, bias, res, y, n_boards, relu, s);
+  return azc::set_error(AZ_ERR_ARG, "az_conv3x3_mx_gpu: channels %d / mode %d unsupported",
+                        channels, mode);
+}
+}  // namespace
+
 extern "C" int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias,
                                  const float* res, float* y, int32_t n_boards,
                                  int32_t channels, int32_t relu, int32_t mode, void* stream) {
+  // 1 board per workgroup measured faster at every shape (profiles/r01_conv_mx.jsonl)
+  return az_conv3x3_mx_cfg_gpu(x, wq, bias, res, y, n_boards, channels, relu, mode, 1, stream);
+}
+
+extern "C" int az_conv3x3_mx_cfg_gpu(const float* x, const void* wq, const float* bias,
+                                     const float* res, float* y, int32_t n_boards,
+                                     int32_t channels, int32_t relu, int32_t mode, int32_t cfg,
+                                     void* stream) {
   AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_mx_gpu: n_boards < 0");
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(x && wq && bias && y && x != y, AZ_ERR_ARG,
              "az_conv3x3_mx_gpu: null buffer or in-place call");
   AZ_REQUIRE(((uintptr_t)x | (uintptr_t)wq | (uintptr_t)bias) % 16 == 0, AZ_ERR_ARG,
              "az_conv3x3_mx_gpu: buffers must be 16-byte aligned");
-  hipStream_t s = azc::as_stream(stream);
-  if (channels == 128 && mode == AZ_CONV_SPLIT3)
-    return launch_mx<Mx<128, AZ_CONV_SPLIT3>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 64 && mode == AZ_CONV_SPLIT3)
-    return launch_mx<Mx<64, AZ_CONV_SPLIT3>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 128 && mode == AZ_CONV_FP16)
-    return launch_mx<Mx<128, AZ_CONV_FP16>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 64 && mode == AZ_CONV_FP16)
-    return launch_mx<Mx<64, AZ_CONV_FP16>>(x, wq, bias, res, y, n_boards, relu, s);
-  return azc::set_error(AZ_ERR_ARG, "az_conv3x3_mx_gpu: channels %d / mode %d unsupported",
-                        channels, mode);
+  AZ_REQUIRE(cfg == 0 || cfg == 1, AZ_ERR_ARG, "az_conv3x3_mx_gpu: cfg %d", cfg);
+  return launch_mx_cfg(x, wq, bias, res, y, n_boards, channels, relu, mode, cfg,
+                       azc::as_stream(stream));
 }

@@ -282,6 +282,11 @@ int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t 
 int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias, const float* res,
                       float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t mode,
                       void* stream);
+/* the same with an explicit workgroup shape (benchmarking): cfg 0 = 2 boards per workgroup
+ * (the default), 1 = 1 board. */
+int az_conv3x3_mx_cfg_gpu(const float* x, const void* wq, const float* bias, const float* res,
+                          float* y, int32_t n_boards, int32_t channels, int32_t relu,
+                          int32_t mode, int32_t cfg, void* stream);
 
 /* AlphaZeroNet's policy and value heads in one kernel (reference Models.py:196-221 with
  * BatchNorm folded, softmax of MCTS_model.py:319): h NHWC float [n_boards, 8, 8, C];

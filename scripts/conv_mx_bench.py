@@ -35,15 +35,17 @@ def run(B, C):
     ms = timed(lambda: nat.lib.az_conv3x3_gpu(*a32))
     out["fp32"] = {"us": round(ms * 1e3, 1), "tf": round(fl / ms / 1e9, 1),
                    "maxerr": float((y.double() - ref).abs().max())}
-    for name, mode in (("split3", nat.AZ_CONV_SPLIT3), ("fp16", nat.AZ_CONV_FP16)):
+    for name, mode, cfg in (("split3", nat.AZ_CONV_SPLIT3, 0), ("split3_1b", nat.AZ_CONV_SPLIT3, 1),
+                            ("fp16", nat.AZ_CONV_FP16, 0), ("fp16_1b", nat.AZ_CONV_FP16, 1)):
         planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
         wq = torch.empty(9 * C * C * planes, dtype=torch.int16, device="cuda")
         nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode, nat.stream_ptr()), "prep")
         y = torch.empty_like(x)
-        args = [nat.ptr(x), nat.ptr(wq), nat.ptr(b), nat.ptr(r), nat.ptr(y), B, C, 1, mode, nat.stream_ptr()]
-        nat.check(nat.lib.az_conv3x3_mx_gpu(*args), name); torch.cuda.synchronize()
+        args = [nat.ptr(x), nat.ptr(wq), nat.ptr(b), nat.ptr(r), nat.ptr(y), B, C, 1, mode, cfg,
+                nat.stream_ptr()]
+        nat.check(nat.lib.az_conv3x3_mx_cfg_gpu(*args), name); torch.cuda.synchronize()
         err = float((y.double() - ref).abs().max())
-        ms = timed(lambda: nat.lib.az_conv3x3_mx_gpu(*args))
+        ms = timed(lambda: nat.lib.az_conv3x3_mx_cfg_gpu(*args))
         out[name] = {"us": round(ms * 1e3, 1), "tf_equiv": round(fl / ms / 1e9, 1), "maxerr": err}
     return out
 
