@@ -37,13 +37,15 @@ def pack_rows(s, device):
 
 
 def unpack_rows(rows):
-    """uint8 [n, ROW_BYTES] -> dict of torch tensors (own/opp int64 bit patterns)."""
-    rows = rows.contiguous()
-    return {"own": rows[:, 0:8].contiguous().view(torch.int64).reshape(-1),
-            "opp": rows[:, 8:16].contiguous().view(torch.int64).reshape(-1),
-            "pi": rows[:, 16:276].contiguous().view(torch.float32),
-            "z": rows[:, 276:284].contiguous().view(torch.float64).reshape(-1),
-            "player": rows[:, 284].contiguous().view(torch.int8)}
+    """uint8 [n, ROW_BYTES] -> dict of torch tensors (own/opp int64 bit patterns).  Each
+    field is cloned before the dtype view: a 1-row or empty slice counts as contiguous
+    and keeps its byte offset, which a wider view rejects."""
+    f = lambda a, b: rows[:, a:b].clone()  # noqa: E731
+    return {"own": f(0, 8).view(torch.int64).reshape(-1),
+            "opp": f(8, 16).view(torch.int64).reshape(-1),
+            "pi": f(16, 276).view(torch.float32),
+            "z": f(276, 284).view(torch.float64).reshape(-1),
+            "player": f(284, 285).view(torch.int8).reshape(-1)}
 
 
 def allgather_samples(s, device, group=None):

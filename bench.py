@@ -14,11 +14,17 @@ selects the plain fp32 MFMA kernel.
 
 A step is one batched simulation over every game slot: select (descent + leaf pack) ->
 net forward -> expand+backup -> move phase; games restart as they finish (weak scaling:
-1,024 games per GPU).  Slots start staggered over the warmup so moves complete at a
-steady rate.  value = (moves completed by all ranks in the timed window / mean plies per
-game of the games completed in the run) / window seconds (the window also contains the
-per-generation RCCL all-gather of the finished games' samples); games that actually
-finished in the window are reported beside it.
+1,024 games per GPU).  Slot starts are staggered over one game length ((sims+1) x 60
+steps) so that when the window opens every slot is playing and the slots' game phases are
+spread evenly over a game (the continuous self-play steady state: end-game simulations are
+cheaper, so a window at one game phase would mis-measure); the untimed warmup runs
+max(W, that stagger) steps to get there (reported as warmup_steps_run).  value = simulations run by all ranks in the
+timed window / (sims per move x mean plies per game of the games completed in the run) /
+window seconds — every move costs exactly `sims` simulations, so this is the game rate,
+and it holds for any window length (a window shorter than one move would see few or no
+move completions).  The window also contains the per-generation RCCL all-gather of the
+finished games' samples.  The move-completion rate and the games that actually finished in
+the window are reported beside it.
 
 Also measured in the same run:
   roofline      the bitboard-step kernel (oth_step_gpu, the north-star kernel) on 2^24
@@ -273,9 +279,11 @@ def main():
                          sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
                          precision=a.conv_precision)
     e = sp.engine
-    # stagger slot starts over the warmup (at least one move length) so moves complete at a
-    # steady rate in the window
-    sp.reset(start_budget=-1, stagger_steps=max(1, min(a.warmup, (a.sims + 1) * 20)))
+    # stagger slot starts over one game length: at the end of the warmup every slot plays
+    # and the game phases are uniform (steady state of continuous self-play)
+    stagger = (a.sims + 1) * int(REF_PLIES_PER_GAME)
+    warmup_run = max(a.warmup, stagger)
+    sp.reset(start_budget=-1, stagger_steps=stagger)
 
     def barrier():
         torch.cuda.synchronize()
@@ -283,7 +291,7 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    sp.step(a.warmup)
+    sp.step(warmup_run)
     barrier()
     c0 = e.counters()
     t0 = time.perf_counter()
@@ -318,18 +326,18 @@ def main():
     plies_all, gtot_all = allst[:, 3].sum(), allst[:, 4].sum()
     t_max = float(allst[:, 5].max())
     plies_per_game = plies_all / gtot_all if gtot_all >= 16 else REF_PLIES_PER_GAME
-    # Every slot always has a game in progress, so moves complete at the steady-state rate
-    # from the first timed step; games/s = that rate / mean plies of the games completed in
-    # the run.  (Completions inside the window follow the staggered start schedule of the
-    # first game generation rather than the steady state, so they are reported, not used.)
-    value = moves_all / plies_per_game / t_max
-    basis = ("moves completed in the window / mean plies per completed game / window "
-             "seconds (all ranks)")
+    # Every slot always has a game in progress and runs one simulation per step; a move is
+    # exactly `sims` simulations, so games/s = simulations/s / (sims x plies per game).
+    # (Game completions inside the window follow the start schedule of the first game
+    # generation rather than the steady state, so they are reported, not used.)
+    value = sims_all / a.sims / plies_per_game / t_max
+    basis = ("simulations in the window / (sims per move x mean plies per completed game) / "
+             "window seconds (all ranks)")
 
     result = {
         "metric": f"self-play games/sec (whole node), 8x8 Othello @ {a.sims} MCTS sims/move",
         "value": round(float(value), 4), "unit": "games/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup,
+        "steps": a.steps, "warmup": a.warmup, "warmup_steps_run": warmup_run,
         "ms_per_step": round(t_max * 1000.0 / a.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": DTYPE_LABEL[a.conv_precision],
         "data": "synthetic: self-play from the initial position, random-init net weights",
@@ -345,7 +353,7 @@ def main():
                    "hip_graph": sp.graph is not None},
         "value_basis": basis,
         "detail": {"moves": int(moves_all),
-                   "game_equivalents_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),
+                   "moves_based_games_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),
                    "simulations": int(sims_all), "plies_per_game": round(float(plies_per_game), 2),
                    "sims_per_s": round(float(sims_all / t_max), 1),
                    "window_s": round(t_max, 3), "allgather_rows": allgather_rows,

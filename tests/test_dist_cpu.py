@@ -73,3 +73,20 @@ def test_replay_allgather_world2_bit_exact():
                 g = g.view(np.uint64)
             assert np.array_equal(g, exp), k
     assert res[0][3] == res[1][3]  # broadcast weights identical on every rank
+
+
+def test_pack_unpack_rows_edge_counts():
+    """0 and 1 rows (a generation in which no / one game finished) round-trip too."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "alphazero-othello_amd"))
+    from dist_replay import pack_rows, unpack_rows
+
+    for n in (0, 1, 2):
+        s = _rows(3, n)
+        got = unpack_rows(pack_rows(s, "cpu"))
+        assert (got["own"].numpy().view(np.uint64) == s["own"]).all()
+        assert (got["opp"].numpy().view(np.uint64) == s["opp"]).all()
+        assert np.array_equal(got["pi"].numpy(), s["pi"])
+        assert np.array_equal(got["z"].numpy(), s["z"])
+        assert np.array_equal(got["player"].numpy(), s["player"])
