@@ -269,6 +269,24 @@ class _HipConv3x3(nn.Module):
             nat.check(rc, "az_conv3x3_mx_gpu")
         return y
 
+    def forward_stem(self, planes, stem, role, x=None):
+        """This conv fused with the stem (`_HipStem`): role 1 = input stem(planes), role 2 =
+        residual stem(planes) (input x); bias + ReLU epilogue (csrc/conv16.hip)."""
+        import az_native as nat
+
+        B = planes.shape[0]
+        y = torch.empty((B, self.channels, 8, 8), dtype=torch.float32, device=planes.device,
+                        memory_format=torch.channels_last)
+        xp = None
+        if role == 2:
+            x = x.contiguous(memory_format=torch.channels_last)
+            xp = nat.ptr(x)
+        nat.check(nat.lib.az_conv3x3_mx_stem_gpu(
+            nat.ptr(planes), nat.ptr(stem.w9), nat.ptr(stem.bias), xp, nat.ptr(self.wq),
+            nat.ptr(self.bias), nat.ptr(y), B, self.channels, role, self.mode,
+            nat.stream_ptr()), "az_conv3x3_mx_stem_gpu")
+        return y
+
 
 class _HipStem(nn.Module):
     """1 -> C 3x3 stem conv + bias + ReLU on the canonical planes (csrc/conv.hip)."""
@@ -335,12 +353,21 @@ class FusedInferenceNet(nn.Module, Inference):
         self.c1 = nn.ModuleList([C3(b.conv1) for b in blocks])
         self.c2 = nn.ModuleList([C3(b.conv2) for b in blocks])
 
+    fuse_stem = True  # the stem evaluated inside the first block's convs (never stored)
+
     def _trunk(self, x):
         if x.dim() == 3:
             x = x.unsqueeze(1)
         x = x.contiguous(memory_format=torch.channels_last)
-        h = self.stem(x)
-        for c1, c2 in zip(self.c1, self.c2):
+        c1s, c2s = list(self.c1), list(self.c2)
+        if (self.fuse_stem and isinstance(self.stem, _HipStem) and c1s
+                and getattr(c1s[0], "precision", "fp32") != "fp32"):
+            planes = x.reshape(x.shape[0], 64).contiguous()
+            h = c2s[0].forward_stem(planes, self.stem, 2, x=c1s[0].forward_stem(planes, self.stem, 1))
+            c1s, c2s = c1s[1:], c2s[1:]
+        else:
+            h = self.stem(x)
+        for c1, c2 in zip(c1s, c2s):
             h = c2(c1(h), res=h)
         return h
 

@@ -145,15 +145,46 @@ __device__ __forceinline__ void mx_sched() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <class G, bool RES, bool RELU>
+// The stem (1 -> C 3x3 conv + bias + ReLU on the canonical planes, k_conv_stem's exact
+// fmaf chain) evaluated where its output is consumed, so it is never written to HBM:
+// STEM = 1: this conv's input is stem(planes) (the first residual block's conv1);
+// STEM = 2: this conv's residual is stem(planes) (that block's conv2).
+struct StemArgs {
+  const float* planes;  // [n_boards][64] float, canonical boards
+  const float* w;       // [9][C]
+  const float* b;       // [C]
+};
+
+// stem output for 4 channels c..c+3 at square p of the staged plane grid `pl` (10 x 10,
+// zero border): same tap order and fmaf chain as k_conv_stem
+__device__ __forceinline__ float4 stem4(const float* pl, int p, int c, int C, StemArgs st) {
+  const int py = p >> 3, px = p & 7;
+  float4 acc = *reinterpret_cast<const float4*>(st.b + c);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+    if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
+      const float v = pl[(yy + 1) * 10 + xx + 1];
+      const float4 wv = *reinterpret_cast<const float4*>(st.w + t * C + c);
+      acc.x = fmaf(v, wv.x, acc.x);
+      acc.y = fmaf(v, wv.y, acc.y);
+      acc.z = fmaf(v, wv.z, acc.z);
+      acc.w = fmaf(v, wv.w, acc.w);
+    }
+  }
+  return make_float4(fmaxf(acc.x, 0.f), fmaxf(acc.y, 0.f), fmaxf(acc.z, 0.f), fmaxf(acc.w, 0.f));
+}
+
+template <class G, bool RES, bool RELU, int STEM>
 __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restrict__ x,
                                                            const char* __restrict__ wq,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ res,
                                                            float* __restrict__ y,
-                                                           int n_boards) {
+                                                           int n_boards, StemArgs st) {
   constexpr int C = G::C, kBoards = G::BOARDS, kThreads = G::THREADS;
   extern __shared__ float4 lds4[];
+  __shared__ float s_plane[kBoards][100];  // STEM: the boards' planes with a zero border
   char* lds_a = reinterpret_cast<char*>(lds4);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -178,13 +209,28 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
     // iteration)
     constexpr int V = (kBoards * 64 + 1) * C / 4;
     constexpr int ITER = (V + kThreads - 1) / kThreads;
+    if (STEM) {
+      for (int i = tid; i < kBoards * 100; i += kThreads) {
+        const int bb = i / 100, q = i % 100, yy = q / 10 - 1, xx = q % 10 - 1;
+        const bool in = bb < nb && (unsigned)yy < 8u && (unsigned)xx < 8u;
+        s_plane[bb][q] = in ? st.planes[(size_t)(b0 + bb) * 64 + yy * 8 + xx] : 0.f;
+      }
+      __syncthreads();
+    }
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
     float4 val[ITER];
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
       const int v = tid + i * kThreads;
       val[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!(AZ_MX_EXP & 4) && v < nb * 64 * (C / 4)) val[i] = src[v];
+      if (STEM == 1) {
+        if (v < nb * 64 * (C / 4)) {
+          const int pos = v / (C / 4);
+          val[i] = stem4(s_plane[pos >> 6], pos & 63, (v % (C / 4)) * 4, C, st);
+        }
+      } else if (!(AZ_MX_EXP & 4) && v < nb * 64 * (C / 4)) {
+        val[i] = src[v];
+      }
     }
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
@@ -274,7 +320,29 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   const int co = col0 + r;
   const float bv = bias[co];
   float rv[G::TM][16];
-  if (RES) {  // all residual loads in flight at once
+  if (RES && STEM == 2) {  // residual = stem(planes) at (row, co), k_conv_stem's fmaf chain
+    float sw[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) sw[t] = st.w[t * C + co];
+    const float sb = st.b[co];
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int m = 32 * mi + (k & 3) + 8 * (k >> 2) + 4 * h;
+        const float* pl = s_plane[(m >> 6) < kBoards ? (m >> 6) : 0];
+        const int py = (m >> 3) & 7, px = m & 7;
+        float a = sb;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+          if ((unsigned)yy < 8u && (unsigned)xx < 8u)
+            a = fmaf(pl[(yy + 1) * 10 + xx + 1], sw[t], a);
+        }
+        rv[mi][k] = fmaxf(a, 0.f);
+      }
+    }
+  } else if (RES) {  // all residual loads in flight at once
 #pragma unroll
     for (int mi = 0; mi < G::TM; ++mi) {
       const size_t o0 = ((size_t)b0 * 64 + 32 * mi + 4 * h) * C + co;
@@ -326,16 +394,16 @@ __global__ void k_conv_mx_prep(const float* __restrict__ w9, uint16_t* __restric
   }
 }
 
-template <class G>
-int launch_mx(const float* x, const void* wq, const float* bias, const float* res, float* y,
-              int n_boards, int relu, hipStream_t s) {
+template <class G, int STEM>
+int launch_mx_t(const float* x, const void* wq, const float* bias, const float* res, float* y,
+                int n_boards, int relu, StemArgs st, hipStream_t s) {
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in once per kernel
   if (!attr_set) {
-    const void* ks[] = {(const void*)k_conv3x3_mx<G, true, true>,
-                        (const void*)k_conv3x3_mx<G, true, false>,
-                        (const void*)k_conv3x3_mx<G, false, true>,
-                        (const void*)k_conv3x3_mx<G, false, false>};
+    const void* ks[] = {(const void*)k_conv3x3_mx<G, true, true, STEM>,
+                        (const void*)k_conv3x3_mx<G, true, false, STEM>,
+                        (const void*)k_conv3x3_mx<G, false, true, STEM>,
+                        (const void*)k_conv3x3_mx<G, false, false, STEM>};
     for (const void* k : ks)
       AZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)G::LDS_BYTES));
@@ -345,15 +413,23 @@ int launch_mx(const float* x, const void* wq, const float* bias, const float* re
   const dim3 blk(G::THREADS);
   const size_t lds = G::LDS_BYTES;
   if (res && relu)
-    hipLaunchKernelGGL((k_conv3x3_mx<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_mx<G, true, true, STEM>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, st);
   else if (res)
-    hipLaunchKernelGGL((k_conv3x3_mx<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_mx<G, true, false, STEM>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, st);
   else if (relu)
-    hipLaunchKernelGGL((k_conv3x3_mx<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_mx<G, false, true, STEM>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, st);
   else
-    hipLaunchKernelGGL((k_conv3x3_mx<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_mx<G, false, false, STEM>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, st);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
+}
+
+template <class G>
+int launch_mx(const float* x, const void* wq, const float* bias, const float* res, float* y,
+              int n_boards, int relu, hipStream_t s, StemArgs st = StemArgs{}, int stem = 0) {
+  if (stem == 1) return launch_mx_t<G, 1>(x, wq, bias, res, y, n_boards, relu, st, s);
+  if (stem == 2) return launch_mx_t<G, 2>(x, wq, bias, res, y, n_boards, relu, st, s);
+  return launch_mx_t<G, 0>(x, wq, bias, res, y, n_boards, relu, st, s);
 }
 
 }  // namespace
@@ -378,22 +454,19 @@ extern "C" int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channel
 
 namespace {
 int launch_mx_cfg(const float* x, const void* wq, const float* bias, const float* res, float* y,
-                  int n_boards, int channels, int relu, int mode, int cfg, hipStream_t s) {
+                  int n_boards, int channels, int relu, int mode, int cfg, hipStream_t s,
+                  StemArgs st = StemArgs{}, int stem = 0) {
   // cfg 0: 2 boards per workgroup (each weight fragment feeds 4 MFMAs); cfg 1: 1 board
   // (half the LDS, 2-3 workgroups per CU, 2 MFMAs per weight fragment)
   const bool two = cfg == 0;
-  if (channels == 128 && mode == AZ_CONV_SPLIT3)
-    return two ? launch_mx<Mx<128, AZ_CONV_SPLIT3, 2>>(x, wq, bias, res, y, n_boards, relu, s)
-               : launch_mx<Mx<128, AZ_CONV_SPLIT3, 1>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 64 && mode == AZ_CONV_SPLIT3)
-    return two ? launch_mx<Mx<64, AZ_CONV_SPLIT3, 2>>(x, wq, bias, res, y, n_boards, relu, s)
-               : launch_mx<Mx<64, AZ_CONV_SPLIT3, 1>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 128 && mode == AZ_CONV_FP16)
-    return two ? launch_mx<Mx<128, AZ_CONV_FP16, 2>>(x, wq, bias, res, y, n_boards, relu, s)
-               : launch_mx<Mx<128, AZ_CONV_FP16, 1>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (channels == 64 && mode == AZ_CONV_FP16)
-    return two ? launch_mx<Mx<64, AZ_CONV_FP16, 2>>(x, wq, bias, res, y, n_boards, relu, s)
-               : launch_mx<Mx<64, AZ_CONV_FP16, 1>>(x, wq, bias, res, y, n_boards, relu, s);
+#define AZ_MX_L(CC, MM)                                                                  \
+  return two ? launch_mx<Mx<CC, MM, 2>>(x, wq, bias, res, y, n_boards, relu, s, st, stem) \
+             : launch_mx<Mx<CC, MM, 1>>(x, wq, bias, res, y, n_boards, relu, s, st, stem);
+  if (channels == 128 && mode == AZ_CONV_SPLIT3) AZ_MX_L(128, AZ_CONV_SPLIT3)
+  if (channels == 64 && mode == AZ_CONV_SPLIT3) AZ_MX_L(64, AZ_CONV_SPLIT3)
+  if (channels == 128 && mode == AZ_CONV_FP16) AZ_MX_L(128, AZ_CONV_FP16)
+  if (channels == 64 && mode == AZ_CONV_FP16) AZ_MX_L(64, AZ_CONV_FP16)
+#undef AZ_MX_L
   return azc::set_error(AZ_ERR_ARG, "az_conv3x3_mx_gpu: channels %d / mode %d unsupported",
                         channels, mode);
 }
@@ -419,4 +492,26 @@ extern "C" int az_conv3x3_mx_cfg_gpu(const float* x, const void* wq, const float
   AZ_REQUIRE(cfg == 0 || cfg == 1, AZ_ERR_ARG, "az_conv3x3_mx_gpu: cfg %d", cfg);
   return launch_mx_cfg(x, wq, bias, res, y, n_boards, channels, relu, mode, cfg,
                        azc::as_stream(stream));
+}
+
+extern "C" int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w,
+                                      const float* stem_b, const float* x, const void* wq,
+                                      const float* bias, float* y, int32_t n_boards,
+                                      int32_t channels, int32_t role, int32_t mode,
+                                      void* stream) {
+  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_mx_stem_gpu: n_boards < 0");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(role == 1 || role == 2, AZ_ERR_ARG, "az_conv3x3_mx_stem_gpu: role %d", role);
+  AZ_REQUIRE(planes && stem_w && stem_b && wq && bias && y && (role == 1 || (x && x != y)),
+             AZ_ERR_ARG, "az_conv3x3_mx_stem_gpu: null buffer or in-place call");
+  AZ_REQUIRE(((uintptr_t)stem_w | (uintptr_t)stem_b | (uintptr_t)wq | (uintptr_t)bias |
+              (uintptr_t)(role == 2 ? x : nullptr)) % 16 == 0,
+             AZ_ERR_ARG, "az_conv3x3_mx_stem_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(channels == 64 || channels == 128, AZ_ERR_ARG,
+             "az_conv3x3_mx_stem_gpu: channels must be 64 or 128");
+  const StemArgs st{planes, stem_w, stem_b};
+  // role 1: input = stem(planes), no residual; role 2: residual = stem(planes) (res is a
+  // non-null placeholder that selects the residual epilogue; it is not read)
+  return launch_mx_cfg(role == 1 ? stem_b : x, wq, bias, role == 2 ? stem_b : nullptr, y,
+                       n_boards, channels, 1, mode, 1, azc::as_stream(stream), st, role);
 }

@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=24000,
                     help="untimed steps; the default (about one game length at 400 sims) lets "
                          "the first games finish so plies/game is measured in this run")
+    ap.add_argument("--warmup-exact", action="store_true",
+                    help="run exactly --warmup untimed steps, not the steady-state minimum "
+                         "(short profiler runs; the value is then not steady state)")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
                     help="BASELINE.json configs: c2 = 4096 games x 100 sims FastOthelloNet; "
                          "c3 = 1024 games x 400 sims AlphaZeroNet(5x128) fp32 (the metric's "
@@ -282,7 +285,7 @@ def main():
     # stagger slot starts over one game length: at the end of the warmup every slot plays
     # and the game phases are uniform (steady state of continuous self-play)
     stagger = (a.sims + 1) * int(REF_PLIES_PER_GAME)
-    warmup_run = max(a.warmup, stagger)
+    warmup_run = a.warmup if a.warmup_exact else max(a.warmup, stagger)
     sp.reset(start_budget=-1, stagger_steps=stagger)
 
     def barrier():

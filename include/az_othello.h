@@ -288,6 +288,18 @@ int az_conv3x3_mx_cfg_gpu(const float* x, const void* wq, const float* bias, con
                           float* y, int32_t n_boards, int32_t channels, int32_t relu,
                           int32_t mode, int32_t cfg, void* stream);
 
+/* az_conv3x3_mx_gpu (1-board workgroups, relu) fused with the stem (1 -> channels 3x3 conv
+ * + bias + ReLU of az_conv_stem_gpu, same fmaf chain, bit-identical) so the stem output is
+ * never stored: role 1 — the input is stem(planes) (x unused, no residual; the first
+ * residual block's conv1); role 2 — the input is x and the residual is stem(planes) (that
+ * block's conv2).  planes float [n_boards][64]; stem_w [9][channels]; stem_b [channels].
+ * Replaces conv0+bn0+relu (Models.py:186-187) / initial_conv (:103-105) plus the first
+ * block's convolutions. */
+int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w, const float* stem_b,
+                           const float* x, const void* wq, const float* bias, float* y,
+                           int32_t n_boards, int32_t channels, int32_t role, int32_t mode,
+                           void* stream);
+
 /* AlphaZeroNet's policy and value heads in one kernel (reference Models.py:196-221 with
  * BatchNorm folded, softmax of MCTS_model.py:319): h NHWC float [n_boards, 8, 8, C];
  * wpv [3][C] (rows: policy ch 0, policy ch 1, value) and bpv [3] the 1x1 convs; wpolT

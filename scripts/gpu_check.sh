@@ -20,7 +20,7 @@ STEPS=${STEPS:-all}
 [[ $STEPS == *pytest* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench 900 python bench.py ${BENCH_ARGS:-}
-[[ $STEPS == *prof* || $STEPS == all ]] && run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --skip-cpu --steps-per-graph 1 ${PROF_ARGS:---steps 400 --warmup 200}
+[[ $STEPS == *prof* || $STEPS == all ]] && run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --skip-cpu --steps-per-graph 1 --warmup-exact ${PROF_ARGS:---steps 400 --warmup 2000}
 [[ $STEPS == *skb* ]] && run skb 120 python scripts/step_kernel_bench.py
 [[ $STEPS == *nnmb* ]] && run nnmb 300 python scripts/nn_microbench.py 1024
 [[ $STEPS == *convb* ]] && run convb 300 python scripts/conv_bench.py

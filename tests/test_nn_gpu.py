@@ -165,3 +165,21 @@ def test_inference_copy_fp16_trunk(kind):
         p, val = fused.evaluate_planes(x)
     torch.testing.assert_close(p, torch.softmax(logits, -1), atol=2e-3, rtol=2e-2)
     torch.testing.assert_close(val, v.reshape(-1), atol=2e-3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("kind", ["az", "fast"])
+@pytest.mark.parametrize("precision", ["split3", "fp16"])
+def test_stem_fusion_is_bit_identical(kind, precision):
+    """The stem evaluated inside the first block's convs (az_conv3x3_mx_stem_gpu) gives the
+    same trunk output bit for bit as the stem kernel + plain convs."""
+    torch.manual_seed(2)
+    net = (AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)).cuda().eval()
+    fused = inference_copy(net, "cuda", precision=precision)
+    x = torch.randint(-1, 2, (131, 1, 8, 8), device="cuda").float()
+    with torch.no_grad():
+        fused.fuse_stem = True
+        a = fused._trunk(x)
+        fused.fuse_stem = False
+        b = fused._trunk(x)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
