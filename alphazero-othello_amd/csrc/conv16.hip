@@ -33,7 +33,8 @@
 
 // experiment hooks (scripts/exp/conv16_exp.py builds copies with bits set): 1 = no A reads
 // in the main loop, 2 = no weight loads in the main loop, 4 = no board staging, 8 = no
-// epilogue stores.  The product build leaves it 0.
+// epilogue stores, 16 = workgroup 0 stamps s_memtime / s_memrealtime around its main loop
+// into y[0..3] (shader clock).  The product build leaves it 0.
 #ifndef AZ_MX_EXP
 #define AZ_MX_EXP 0
 #endif
@@ -284,6 +285,8 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   // MFMA pipe then idles while they issue) or sink them behind; mx_sched pins the issue
   // pattern: each LDS read in the shadow of two MFMAs, the weight loads behind the MFMAs.
   static_assert(G::CHUNKS % 4 == 0, "B ring of 4 and A ring of 2 within a tap");
+  const uint64_t clk0 = (AZ_MX_EXP & 16) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt0 = (AZ_MX_EXP & 16) ? __builtin_amdgcn_s_memrealtime() : 0;
   AFrag<G> a0f, a1f;
   int bcur[G::TM], bnxt[G::TM];
   mx_tap_base<G>(bcur, 0, pos0, ok9, h);
@@ -314,6 +317,12 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
     for (int mi = 0; mi < G::TM; ++mi) bcur[mi] = bnxt[mi];
   }
 #undef AZ_MX_STEP
+  if ((AZ_MX_EXP & 16) && blockIdx.x == 0 && tid == 0) {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<uint64_t*>(y)[0] = clk1 - clk0;
+    reinterpret_cast<uint64_t*>(y)[1] = rt1 - rt0;
+    return;
+  }
 
   // ---- epilogue: D[row][col], col = lane&31, row = (k&3) + 8*(k>>2) + 4*(lane>>5); a
   // 32-row tile lies inside one board, so the tail-board test is uniform per tile

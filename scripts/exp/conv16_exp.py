@@ -8,9 +8,10 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 SRC = os.path.join(ROOT, "alphazero-othello_amd", "csrc", "conv16.hip")
 out = {}
 B, C = 1024, 128
-x = torch.randn(B, C, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)
+x = torch.randn(B, C, 8, 8, device="cuda").relu().contiguous(memory_format=torch.channels_last)
 r = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
 wq = torch.zeros(9 * C * C * 3, dtype=torch.int16, device="cuda")
+w9 = (torch.randn(9, C, C, device="cuda") / (3 * C ** 0.5)).contiguous()
 b = torch.zeros(C, device="cuda")
 y = torch.empty_like(x)
 for exp in [int(v) for v in os.environ.get("EXPS", "0,1,2,3,4,8,12,15").split(",")]:
@@ -19,6 +20,9 @@ for exp in [int(v) for v in os.environ.get("EXPS", "0,1,2,3,4,8,12,15").split(",
                            "-std=c++17", "-ffp-contract=off", f"-DAZ_MX_EXP={exp}", SRC,
                            os.path.join(ROOT, "alphazero-othello_amd", "csrc", "board.hip"), "-o", so])
     L = ctypes.CDLL(so)
+    if os.environ.get("RANDOM_W"):
+        assert L.az_conv3x3_mx_prep_gpu(ctypes.c_void_p(w9.data_ptr()), ctypes.c_void_p(wq.data_ptr()), C, 0,
+                                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
     args = [ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wq.data_ptr()), ctypes.c_void_p(b.data_ptr()),
             ctypes.c_void_p(r.data_ptr()), ctypes.c_void_p(y.data_ptr()), B, C, 1, 0,
             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)]
@@ -33,4 +37,8 @@ for exp in [int(v) for v in os.environ.get("EXPS", "0,1,2,3,4,8,12,15").split(",
             L.az_conv3x3_mx_gpu(*args)
         e1.record(); torch.cuda.synchronize()
         out[f"exp{exp}_mode{mode}"] = round(e0.elapsed_time(e1) / 30 * 1e3, 1)
+        if exp & 16:
+            st = torch.as_strided(y, (4,), (1,)).clone().view(torch.int64)[:2].cpu().numpy()
+            out[f"exp{exp}_mode{mode}_clockGHz"] = round(float(st[0]) / float(st[1]) * 0.1, 3)
+            out[f"exp{exp}_mode{mode}_loop_us"] = round(float(st[1]) / 100.0, 1)
     print(json.dumps(out), flush=True)
