@@ -94,8 +94,9 @@ struct Counters {  // device-side, 64-bit
   unsigned long long sims;
   unsigned long long moves;
   long long start_budget;  // games still allowed to start (refill)
-  int32_t ready_n;
+  int32_t ready_n;         // slots whose search finished this step (k_move's work list)
   int32_t unlimited;       // refill without a start budget
+  int32_t move_done;       // k_move workgroups finished this step (the last one resets)
 };
 
 struct Samples {
@@ -829,8 +830,16 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
     __syncthreads();
   }
   __syncthreads();
-  if (blockIdx.x == 0 && tid == 0) {
-    p.ctr->step += 1;
+  // the last workgroup to finish (every workgroup has read ready_n by then) clears the
+  // work list for the next step and advances the step counter: no separate memset launch
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(&p.ctr->move_done, 1) == (int)gridDim.x - 1) {
+      p.ctr->ready_n = 0;
+      p.ctr->move_done = 0;
+      p.ctr->step += 1;
+      __threadfence();
+    }
   }
 }
 
@@ -852,6 +861,7 @@ __global__ void k_reset(Params p, long long budget, int stagger) {
     p.ctr->sims = 0;
     p.ctr->moves = 0;
     p.ctr->ready_n = 0;
+    p.ctr->move_done = 0;
   }
   if (g >= p.G) return;
   p.g.half[g] = 0;
@@ -1272,7 +1282,6 @@ int az_begin_search(az_engine* e, int32_t slot, int32_t num_simulations, void* s
 int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
   AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select: null argument");
   hipStream_t s = azc::as_stream(stream);
-  AZ_HIP(hipMemsetAsync(&e->p.ctr->ready_n, 0, sizeof(int32_t), s));
   // Simulations that end on a terminal node need no evaluation and run inside the select
   // call; cap them per step so one end-game tree (every simulation terminal) cannot hold
   // the whole batched step for hundreds of dependent descents.  Host-driven engines step

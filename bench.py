@@ -56,6 +56,7 @@ SELFPLAY_ARGS = {"c_puct": 2.0, "num_simulations": 400, "dirichlet_alpha": 1.0,
                  "num_exploratory_moves": 35, "lambda": 0.98}
 REF_PLIES_PER_GAME = 60.0  # SURVEY.md 6 (measured on the reference at 400 sims)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0      # the guide's measured float4 copy rate (MI355X_MICROARCH.md)
 STEP_BYTES = 43            # algorithmic bytes per board step
 MFMA16_PEAK = 2500.0       # dense bf16 / fp16 MFMA TFLOP/s (MI355X_MICROARCH.md)
 MFMA32_PEAK = 157.3        # dense fp32 MFMA TFLOP/s
@@ -378,6 +379,7 @@ def main():
         result["roofline"] = {"kernel": "oth_step_gpu (k_step)", "bound": "hbm",
                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                              "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
                               "traffic": traffic, "positions": n,
                               "avg_launch_ms": round(ms, 4),
                               "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
