@@ -112,6 +112,7 @@ SIGNATURES = {
     "az_heads_az_gpu": [_P] * 11 + [_I32, _I32, _P],
     "az_conv3x3_mx_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_stem_gpu": [_P] * 7 + [_I32, _I32, _I32, _I32, _P],
+    "az_replay_aggregate_gpu": [_P] * 5 + [_I64] + [_P] * 10,
 }
 
 

@@ -300,6 +300,21 @@ int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w, const float
                            int32_t n_boards, int32_t channels, int32_t role, int32_t mode,
                            void* stream);
 
+/* ---------------- replay buffer (device) -------------------------------------------
+ * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with
+ * equal (own, opp, version) — the reference's (sha1(canonical int8 board), version) —
+ * collapse to one sample, emitted in order of first occurrence: pi_o = mean pi
+ * normalised by (its NumPy-pairwise sum + 1e-12) in float32, v_o = float32(mean v),
+ * count_o = group size; *n_out (device int32) = number of samples.  Inputs: own/opp
+ * [n], ver [n], pi [n][65] float, v [n] double.  Outputs sized n (the upper bound).
+ * Call with workspace = NULL to get *workspace_bytes, then again with that much device
+ * memory.  Asynchronous on `stream`. */
+int az_replay_aggregate_gpu(const uint64_t* own, const uint64_t* opp, const int32_t* ver,
+                            const float* pi, const double* v, int64_t n, uint64_t* own_o,
+                            uint64_t* opp_o, int32_t* ver_o, float* pi_o, float* v_o,
+                            int32_t* count_o, int32_t* n_out, void* workspace,
+                            size_t* workspace_bytes, void* stream);
+
 /* AlphaZeroNet's policy and value heads in one kernel (reference Models.py:196-221 with
  * BatchNorm folded, softmax of MCTS_model.py:319): h NHWC float [n_boards, 8, 8, C];
  * wpv [3][C] (rows: policy ch 0, policy ch 1, value) and bpv [3] the 1x1 convs; wpolT

@@ -28,6 +28,10 @@ pos = squares holding +1, neg = squares holding -1 of the absolute-colour state)
                       trajectories with passes, lambda in {0.98, 1.0}.
   tictactoe_stats.json outcome distribution of rollout self-play on a copy-on-step
                       TicTacToe (statistical pin only).
+  replay_aggregate.npz reference Trainer._aggregate_duplicates (train.py:142-173) on a
+                      synthetic replay buffer with duplicate boards within and across
+                      model versions: inputs and the (state, mean pi, mean v) outputs in
+                      the reference's first-occurrence order.
 """
 import json
 import os
@@ -556,7 +560,61 @@ def gen_tictactoe():
     print("tictactoe:", outcomes)
 
 
-GENS = {"board": gen_board, "bitboard": gen_bitboard, "edge": gen_edge, "d4": gen_d4,
+# ----------------------------------------------------------------------------------------
+def gen_replay():
+    import train
+
+    rng = np.random.default_rng(33)
+    d = np.load(os.path.join(HERE, "board_corpus.npz"))
+    # a small pool of reachable canonical boards so that duplicates are common, plus the
+    # initial position (present in every game of a generation)
+    pool_idx = rng.choice(len(d["pos"]), size=300, replace=False)
+    pool = [(int(d["pos"][i]), int(d["neg"][i])) for i in pool_idx]
+    pool.append((0x0000000810000000, 0x0000001008000000))
+    w = np.uint64(1) << np.arange(64, dtype=np.uint64)
+
+    def board(pos, neg):
+        b = np.zeros(64, np.int8)
+        b[(np.uint64(pos) & w) != 0] = 1
+        b[(np.uint64(neg) & w) != 0] = -1
+        return b.reshape(8, 8)
+
+    n = 4000
+    rows = []
+    for _ in range(n):
+        k = len(pool) - 1 if rng.random() < 0.1 else int(rng.integers(0, len(pool) // 3)) \
+            if rng.random() < 0.6 else int(rng.integers(0, len(pool)))
+        pi = rng.random(65).astype(np.float32)
+        pi[rng.random(65) < 0.7] = 0.0
+        pi[int(rng.integers(0, 65))] += np.float32(0.5)
+        pi /= pi.sum()
+        v = float(rng.uniform(-1, 1))
+        ver = int(rng.integers(0, 3))
+        rows.append((board(*pool[k]), pi.astype(np.float32), v, ver, pool[k]))
+
+    class Fake:
+        pass
+
+    fake = Fake()
+    fake.replay_buffer = [(r[0], r[1], r[2], r[3]) for r in rows]
+    fake._hash_state = lambda b: train.Trainer._hash_state(fake, b)
+    states, policies, values = train.Trainer._aggregate_duplicates(fake)
+    out_pos = np.array([int(np.bitwise_or.reduce(np.where(s.reshape(-1) == 1, w, np.uint64(0))))
+                        for s in states], np.uint64)
+    out_neg = np.array([int(np.bitwise_or.reduce(np.where(s.reshape(-1) == -1, w, np.uint64(0))))
+                        for s in states], np.uint64)
+    np.savez_compressed(
+        os.path.join(HERE, "replay_aggregate.npz"),
+        in_pos=np.array([r[4][0] for r in rows], np.uint64),
+        in_neg=np.array([r[4][1] for r in rows], np.uint64),
+        in_pi=np.stack([r[1] for r in rows]), in_v=np.array([r[2] for r in rows], np.float64),
+        in_ver=np.array([r[3] for r in rows], np.int32),
+        out_pos=out_pos, out_neg=out_neg, out_pi=np.stack(policies),
+        out_v=np.array(values, np.float32))
+    print("replay_aggregate:", n, "rows ->", len(states), "buckets")
+
+
+GENS = {"replay": gen_replay, "board": gen_board, "bitboard": gen_bitboard, "edge": gen_edge, "d4": gen_d4,
         "mcts": gen_mcts, "selfplay": gen_selfplay, "training": gen_training_data,
         "tictactoe": gen_tictactoe}
 

@@ -166,3 +166,17 @@ def test_mock_policy_is_float32_exact():
     assert p.dtype == np.float32
     assert (p * 1024 == np.rint(p * 1024)).all()
     assert (np.float32(v).astype(np.float64) == v).all()
+
+
+def test_replay_aggregate_oracle_matches_reference():
+    """oracle/replay.py against the reference's Trainer._aggregate_duplicates output
+    (train.py:142-173), bit for bit, order included."""
+    from oracle import replay
+
+    d = load_golden("replay_aggregate.npz")
+    own, opp, ver, pi, v, cnt = replay.aggregate(d["in_pos"], d["in_neg"], d["in_ver"],
+                                                 d["in_pi"], d["in_v"])
+    assert (own == d["out_pos"]).all() and (opp == d["out_neg"]).all()
+    assert np.array_equal(pi, d["out_pi"])
+    assert np.array_equal(v, d["out_v"])
+    assert cnt.sum() == len(d["in_pos"])
