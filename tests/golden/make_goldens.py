@@ -28,6 +28,8 @@ pos = squares holding +1, neg = squares holding -1 of the absolute-colour state)
                       trajectories with passes, lambda in {0.98, 1.0}.
   tictactoe_stats.json outcome distribution of rollout self-play on a copy-on-step
                       TicTacToe (statistical pin only).
+  augment.npz         reference envs.othello.get_random_symmetry (envs/othello.py:501-526)
+                      on canonical boards + policies, with the (k, flip) it drew.
   replay_aggregate.npz reference Trainer._aggregate_duplicates (train.py:142-173) on a
                       synthetic replay buffer with duplicate boards within and across
                       model versions: inputs and the (state, mean pi, mean v) outputs in
@@ -614,7 +616,39 @@ def gen_replay():
     print("replay_aggregate:", n, "rows ->", len(states), "buckets")
 
 
-GENS = {"replay": gen_replay, "board": gen_board, "bitboard": gen_bitboard, "edge": gen_edge, "d4": gen_d4,
+# ----------------------------------------------------------------------------------------
+def gen_augment():
+    from envs.othello import get_random_symmetry
+
+    rng = np.random.default_rng(44)
+    d = np.load(os.path.join(HERE, "board_corpus.npz"))
+    sel = rng.choice(len(d["pos"]), size=512, replace=False)
+    w = np.uint64(1) << np.arange(64, dtype=np.uint64)
+    pos, neg = d["pos"][sel].astype(np.uint64), d["neg"][sel].astype(np.uint64)
+    states = np.zeros((len(sel), 64), np.float32)
+    states[(pos[:, None] & w) != 0] = 1.0
+    states[(neg[:, None] & w) != 0] = -1.0
+    states = states.reshape(-1, 8, 8)
+    pis = rng.random((len(sel), 65)).astype(np.float32)
+    pis /= pis.sum(1, keepdims=True)
+    np.random.seed(123)
+    outs_s, outs_p = [], []
+    for i in range(len(sel)):
+        s_out, p_out = get_random_symmetry(states[i], pis[i])
+        outs_s.append(s_out)
+        outs_p.append(p_out)
+    np.random.seed(123)  # the same draws, recorded: k = randint(4), flip = rand() < 0.5
+    ks, flips = [], []
+    for i in range(len(sel)):
+        ks.append(np.random.randint(4))
+        flips.append(np.random.rand() < 0.5)
+    np.savez_compressed(os.path.join(HERE, "augment.npz"), pos=pos, neg=neg, pi=pis,
+                        k=np.array(ks, np.int32), flip=np.array(flips, np.int32),
+                        out_state=np.stack(outs_s), out_pi=np.stack(outs_p))
+    print("augment:", len(sel))
+
+
+GENS = {"augment": gen_augment, "replay": gen_replay, "board": gen_board, "bitboard": gen_bitboard, "edge": gen_edge, "d4": gen_d4,
         "mcts": gen_mcts, "selfplay": gen_selfplay, "training": gen_training_data,
         "tictactoe": gen_tictactoe}
 

@@ -198,3 +198,20 @@ def test_cpu_step_random_positions_vs_oracle():
     assert (st == rs).all()
     assert (o == ro).all() and (p == rp).all() and (lg == rl).all()
     assert (nat.legal_cpu(own, opp) == ob.legal_batch(own, opp)).all()
+
+
+def test_augment_tables_match_reference_get_random_symmetry():
+    """The pi permutation tables of train_gpu (built from the bitboard D4 map) reproduce the
+    reference's get_random_symmetry (envs/othello.py:501-526) for the (k, flip) it drew."""
+    from train_gpu import pi_source_tables
+
+    d = load_golden("augment.npz")
+    src = pi_source_tables()
+    sym = d["k"] + 4 * d["flip"]
+    assert np.array_equal(np.take_along_axis(d["pi"], src[sym], 1), d["out_pi"])
+    w = np.uint64(1) << np.arange(64, dtype=np.uint64)
+    for i in range(len(sym)):
+        o = nat.d4_cpu(d["pos"][i:i + 1], int(sym[i]))[0]
+        p = nat.d4_cpu(d["neg"][i:i + 1], int(sym[i]))[0]
+        plane = ((o & w) != 0).astype(np.float32) - ((p & w) != 0).astype(np.float32)
+        assert np.array_equal(plane.reshape(1, 8, 8), d["out_state"][i])
