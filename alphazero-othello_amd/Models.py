@@ -6,6 +6,7 @@ only dense contractions on the path.  `Inference.inference` keeps the reference'
 host API (Models.py:11-31); `evaluate_planes` is what the batched self-play engine calls
 on the [G, 64] canonical planes it packs on device.
 """
+import os
 from typing import Tuple
 
 import numpy as np
@@ -149,19 +150,21 @@ def get_config(net):
 
 
 def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
-                   conv="hip", precision=None) -> nn.Module:
+                   conv="hip", precision=None, conv_algo=None) -> nn.Module:
     """An eval-mode copy of `net` on `device` for the batched engine: BatchNorm folded
     into the preceding convolution (same function in eval mode, fewer kernels per step).
     With `fused` (AlphaZeroNet / FastOthelloNet) the convolutions run without bias and one
     HIP epilogue applies bias + residual + ReLU.  conv="hip" runs the 3x3 trunk on the
     fused MFMA kernels, in `precision`:
       "split3" (default for fp32): bf16x3-split operands on the 16-bit MFMA pipe, six
-               partial products accumulated in fp32 — fp32-accurate (csrc/conv16.hip;
-               tests/test_nn_gpu.py bounds its error by the fp32 kernel's against fp64);
+               partial products accumulated in fp32 — fp32-accurate (csrc/conv16.hip, or
+               at 128 channels the Winograd F(2x2,3x3) form csrc/conv_wino.hip;
+               tests/test_nn_gpu.py bounds both errors by the fp32 kernel's against fp64);
       "fp32":  fp32 MFMA (csrc/conv.hip);
       "fp16":  fp16 operands, fp32 accumulation (config #5's fp16 inference; the default
                when dtype is float16).
-    Activations, the stem and the heads stay fp32 on the fused path."""
+    Activations, the stem and the heads stay fp32 on the fused path.  conv_algo ("direct" /
+    "wino") overrides default_conv_algo for the 16-bit trunk."""
     if precision is None:
         precision = "fp16" if dtype == torch.float16 else "split3"
     assert precision in ("split3", "fp32", "fp16"), precision
@@ -192,7 +195,7 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
     m = m.to(device=device, dtype=torch.float32 if fusable else dtype)
     m = m.to(memory_format=torch.channels_last)
     if fusable:
-        return FusedInferenceNet(m, conv=conv, precision=precision).eval()
+        return FusedInferenceNet(m, conv=conv, precision=precision, conv_algo=conv_algo).eval()
     return m.eval()
 
 
@@ -221,14 +224,26 @@ class _ConvEpilogue(nn.Module):
         return y
 
 
+def default_conv_algo(precision, channels):
+    """The 16-bit-pipe 3x3 conv algorithm: "wino" (csrc/conv_wino.hip, Winograd F(2x2,3x3))
+    where it measured faster (split3, 128 channels: profiles/r01_conv_mx.jsonl), "direct"
+    (csrc/conv16.hip) elsewhere; AZ_CONV_ALGO=direct|wino overrides."""
+    env = os.environ.get("AZ_CONV_ALGO")
+    if env in ("direct", "wino"):
+        return env
+    return "wino" if precision == "split3" and channels == 128 else "direct"
+
+
 class _HipConv3x3(nn.Module):
     """3x3 conv (Ci = Co in {64, 128}) + bias (+ residual) + ReLU in one MFMA kernel:
     precision "fp32" = csrc/conv.hip (weights re-laid [tap][Co][Ci]); "split3" / "fp16" =
-    csrc/conv16.hip (weights split once into 16-bit planes by az_conv3x3_mx_prep_gpu)."""
+    csrc/conv16.hip (algo "direct": weights split once into 16-bit planes by
+    az_conv3x3_mx_prep_gpu) or csrc/conv_wino.hip (algo "wino": weights transformed to the
+    Winograd domain and split by az_conv3x3_wino_prep_gpu)."""
 
     MODES = {"split3": 0, "fp16": 1}  # AZ_CONV_SPLIT3, AZ_CONV_FP16
 
-    def __init__(self, conv: nn.Conv2d, precision="split3"):
+    def __init__(self, conv: nn.Conv2d, precision="split3", algo=None):
         super().__init__()
         import az_native as nat
 
@@ -237,6 +252,7 @@ class _HipConv3x3(nn.Module):
         assert co == ci and co in (64, 128) and w.shape[2:] == (3, 3)
         self.channels = co
         self.precision = precision
+        self.algo = "direct" if precision == "fp32" else (algo or default_conv_algo(precision, co))
         w9 = w.float().permute(2, 3, 0, 1).reshape(9, co, ci).contiguous()
         self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
         if precision == "fp32":
@@ -244,9 +260,11 @@ class _HipConv3x3(nn.Module):
         else:
             self.mode = self.MODES[precision]
             planes = 3 if precision == "split3" else 1
-            wq = torch.empty(9 * co * ci * planes, dtype=torch.int16, device=w.device)
-            nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(wq), co, self.mode,
-                                                     nat.stream_ptr()), "az_conv3x3_mx_prep_gpu")
+            taps = 16 if self.algo == "wino" else 9
+            wq = torch.empty(taps * co * ci * planes, dtype=torch.int16, device=w.device)
+            prep = nat.lib.az_conv3x3_wino_prep_gpu if self.algo == "wino" else nat.lib.az_conv3x3_mx_prep_gpu
+            nat.check(prep(nat.ptr(w9), nat.ptr(wq), co, self.mode, nat.stream_ptr()),
+                      "conv3x3 weight prep")
             self.wq = nn.Parameter(wq, requires_grad=False)
 
     def forward(self, x, res=None, relu=True):
@@ -263,10 +281,10 @@ class _HipConv3x3(nn.Module):
                                         nat.stream_ptr())
             nat.check(rc, "az_conv3x3_gpu")
         else:
-            rc = nat.lib.az_conv3x3_mx_gpu(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp,
-                                           nat.ptr(y), x.shape[0], self.channels, int(relu),
-                                           self.mode, nat.stream_ptr())
-            nat.check(rc, "az_conv3x3_mx_gpu")
+            fn = nat.lib.az_conv3x3_wino_gpu if self.algo == "wino" else nat.lib.az_conv3x3_mx_gpu
+            rc = fn(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp, nat.ptr(y), x.shape[0],
+                    self.channels, int(relu), self.mode, nat.stream_ptr())
+            nat.check(rc, "az_conv3x3_wino_gpu" if self.algo == "wino" else "az_conv3x3_mx_gpu")
         return y
 
     def forward_stem(self, planes, stem, role, x=None):
@@ -327,7 +345,7 @@ class FusedInferenceNet(nn.Module, Inference):
 
     input_dtype = torch.float32
 
-    def __init__(self, m: nn.Module, conv="hip", precision="split3"):
+    def __init__(self, m: nn.Module, conv="hip", precision="split3", conv_algo=None):
         super().__init__()
         self.conv_impl = conv
         self.precision = precision
@@ -335,7 +353,7 @@ class FusedInferenceNet(nn.Module, Inference):
         self.board_size = m.board_size
         self.softmax = nn.Softmax(dim=-1)
         if conv == "hip":
-            C3 = lambda c: _HipConv3x3(c, precision)  # noqa: E731
+            C3 = lambda c: _HipConv3x3(c, precision, conv_algo)  # noqa: E731
         else:
             C3 = _ConvEpilogue
         Stem = _HipStem if conv == "hip" else _ConvEpilogue
@@ -361,7 +379,8 @@ class FusedInferenceNet(nn.Module, Inference):
         x = x.contiguous(memory_format=torch.channels_last)
         c1s, c2s = list(self.c1), list(self.c2)
         if (self.fuse_stem and isinstance(self.stem, _HipStem) and c1s
-                and getattr(c1s[0], "precision", "fp32") != "fp32"):
+                and getattr(c1s[0], "precision", "fp32") != "fp32"
+                and c1s[0].algo == "direct" and c2s[0].algo == "direct"):
             planes = x.reshape(x.shape[0], 64).contiguous()
             h = c2s[0].forward_stem(planes, self.stem, 2, x=c1s[0].forward_stem(planes, self.stem, 1))
             c1s, c2s = c1s[1:], c2s[1:]

@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["csrc/board.hip", "csrc/engine.hip", "csrc/nn_fused.hip", "csrc/conv.hip", "csrc/conv16.hip", "csrc/heads.hip", "csrc/replay.hip"]
+SOURCES = ["csrc/board.hip", "csrc/engine.hip", "csrc/nn_fused.hip", "csrc/conv.hip", "csrc/conv16.hip", "csrc/conv_wino.hip", "csrc/heads.hip", "csrc/replay.hip"]
 HEADERS = ["csrc/bitboard.h", "csrc/common.h", "csrc/philox.h", "../include/az_othello.h"]
 OUT = os.path.join(HERE, "libaz_othello.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",

@@ -39,6 +39,7 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kSelBlock = 256;  // 4 slots (waves) per workgroup in select / expand
 constexpr int kMoveBlock = 256;
+constexpr int kMaxPath = 64;     // one wave lane per path depth for the parallel backup
 
 enum : uint8_t { kExpanded = 1, kTerminal = 2, kChildF64 = 4 };
 enum : int32_t { kIdle = AZ_GAME_IDLE, kActive = AZ_GAME_ACTIVE, kFinished = AZ_GAME_FINISHED,
@@ -67,6 +68,8 @@ struct Games {
   int32_t* sims_done;
   int32_t* sims_target;
   int32_t* leaf;       // leaf awaiting evaluation, -1 none
+  int32_t* path;       // [G, kMaxPath] root..leaf node indices of the pending leaf
+  int32_t* path_len;   // entries in `path`; 0 => deeper than kMaxPath, walk parents
   int32_t* ply;
   int32_t* root_player;
   int32_t* winner;
@@ -192,6 +195,21 @@ __device__ void backup(const Params& p, int g, int half, int node, double v) {
   }
 }
 
+// The same update with the path held one node per lane (lane d = depth d, leaf at depth
+// `leaf_depth` < kMaxPath): every node's N/W is read and written in one round trip instead
+// of one dependent parent load per level.  W += (+/-1)*v is the identical double addition.
+__device__ void backup_path(const Params& p, int g, int half, int path_node, int leaf_depth,
+                            double v) {
+  const int lane = lane_id();
+  if (lane <= leaf_depth) {
+    const int64_t k = nidx(p, half, g, path_node);
+    const int n = p.a.N[k];
+    const double w = p.a.W[k];
+    p.a.N[k] = n + 1;
+    p.a.W[k] = w + (((leaf_depth - lane) & 1) ? -v : v);
+  }
+}
+
 // Pack the canonical NN input player*state (Models.py:16): own stones +1, opponent -1,
 // optionally through D4 transform `sym` (random_symmetry, MCTS_model.py:15-28).
 __device__ void emit_leaf(const Params& p, float* nn_in, int g, uint64_t own, uint64_t opp,
@@ -207,26 +225,54 @@ __device__ void emit_none(float* nn_in, int32_t* leaf_o, int g) {
   if (lane_id() == 0 && leaf_o) leaf_o[g] = -1;
 }
 
+// What the descent needs of a node, loaded together with its siblings' PUCT inputs so that
+// one round trip per tree level suffices.
+struct NodeRec {
+  int node;
+  int first;   // first child
+  int visits;  // N
+  int meta;    // flags | nchild << 8 | (uint8)tval << 16
+};
+
+__device__ __forceinline__ NodeRec load_rec(const Params& p, int g, int half, int node) {
+  const int64_t k = nidx(p, half, g, node);
+  NodeRec r;
+  r.node = node;
+  r.first = p.a.first[k];
+  r.visits = p.a.N[k];
+  r.meta = (int)p.a.flags[k] | ((int)p.a.nchild[k] << 8) | ((int)(uint8_t)p.a.tval[k] << 16);
+  return r;
+}
+__device__ __forceinline__ uint8_t rec_flags(const NodeRec& r) { return (uint8_t)r.meta; }
+__device__ __forceinline__ int rec_nchild(const NodeRec& r) { return (r.meta >> 8) & 0xff; }
+__device__ __forceinline__ int rec_tval(const NodeRec& r) { return (int)(int8_t)(r.meta >> 16); }
+
 // PUCT child choice of MCTS._select_child / Node._get_ucb_score (MCTS_model.py:129-139,
 // :362-370).  NumPy-2 promotion: with float32 priors every operation after the Python-float
 // sqrt is float32 (c_puct and q are cast to float32); with the Dirichlet-noised root's
 // float64 priors it is all float64.  The node's own virtual visit (+1, MCTS_model.py:378)
 // enters the sqrt; the children carry none.  max() keeps the first maximum in ascending
 // action order, i.e. the lowest child index.
-__device__ int select_child(const Params& p, int g, int half, int node) {
+// The parent's record is already in registers, each lane
+// loads its child's PUCT inputs AND its record, and the winner's record is broadcast from
+// its lane -- the next level starts without another load.
+__device__ NodeRec select_child_rec(const Params& p, int g, int half, const NodeRec& par) {
   const int lane = lane_id();
-  const int64_t k = nidx(p, half, g, node);
-  const int nc = p.a.nchild[k];
-  const int fc = p.a.first[k];
-  const bool f64 = (p.a.flags[k] & kChildF64) != 0;
-  const double sq = sqrt((double)(p.a.N[k] + 1) + 1e-8);
+  const int nc = rec_nchild(par);
+  const int fc = par.first;
+  const bool f64 = (rec_flags(par) & kChildF64) != 0;
+  const double sq = sqrt((double)(par.visits + 1) + 1e-8);
   double score = -INFINITY;
   int idx = 0x7fffffff;
+  NodeRec mine{0, 0, 0, 0};
   if (lane < nc) {
     const int64_t c = nidx(p, half, g, fc + lane);
     const int n = p.a.N[c];
     const double w = p.a.W[c];
     const double pr = p.a.P[c];
+    mine.first = p.a.first[c];
+    mine.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
+    mine.visits = n;
     const double q = -(n == 0 ? 0.0 : w / (double)n);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + n);
@@ -246,7 +292,12 @@ __device__ int select_child(const Params& p, int g, int half, int node) {
       idx = oi;
     }
   }
-  return fc + idx;
+  NodeRec r;
+  r.node = fc + idx;
+  r.first = __shfl(mine.first, idx, kWave);
+  r.visits = __shfl(mine.visits, idx, kWave);
+  r.meta = __shfl(mine.meta, idx, kWave);
+  return r;
 }
 
 __device__ void push_ready(const Params& p, int g) {
@@ -272,30 +323,40 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   const int half = p.g.half[g];
   int sims_done = p.g.sims_done[g];
   const int target = p.g.sims_target[g];
-  const int64_t root = nidx(p, half, g, 0);
   int leaf = -1;
-  if (!(p.a.flags[root] & kExpanded)) {
+  int depth = 0;      // depth of the current node
+  int path_node = 0;  // lane d: node at depth d of the current descent
+  NodeRec cur = load_rec(p, g, half, 0);
+  if (!(rec_flags(cur) & kExpanded)) {
     leaf = 0;  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
   } else {
     int guard = 0;
     while (sims_done < target && guard < max_descents) {
+      if (guard > 0) cur = load_rec(p, g, half, 0);  // the last backup changed the root's N
       ++guard;
-      int node = 0;
+      depth = 0;
+      path_node = 0;
       bool done = false;
       while (!done) {
-        const int64_t k = nidx(p, half, g, node);
-        const uint8_t f = p.a.flags[k];
+        const uint8_t f = rec_flags(cur);
         if (f & kTerminal) {  // MCTS_model.py:381-384
-          if (lane == 0) backup(p, g, half, node, (double)p.a.tval[k]);
-          // lane 0's N/W stores must be visible to the wave's next PUCT loads
+          const double tv = (double)rec_tval(cur);
+          if (depth < kMaxPath) {
+            backup_path(p, g, half, path_node, depth, tv);
+          } else if (lane == 0) {
+            backup(p, g, half, cur.node, tv);
+          }
+          // the N/W stores must be visible to the wave's next PUCT loads
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
           ++sims_done;
           done = true;
         } else if (!(f & kExpanded)) {  // MCTS_model.py:386-389
-          leaf = node;
+          leaf = cur.node;
           done = true;
         } else {
-          node = select_child(p, g, half, node);
+          cur = select_child_rec(p, g, half, cur);
+          ++depth;
+          if (lane == depth) path_node = cur.node;
         }
       }
       if (leaf >= 0) break;
@@ -313,7 +374,9 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       }
     }
     emit_leaf(p, nn_in, g, p.a.own[k], p.a.opp[k], sym);
+    if (depth < kMaxPath && lane <= depth) p.g.path[(int64_t)g * kMaxPath + lane] = path_node;
     if (lane == 0) {
+      p.g.path_len[g] = depth < kMaxPath ? depth + 1 : 0;
       p.g.leaf[g] = leaf;
       if (leaf_o) leaf_o[g] = leaf;
     }
@@ -491,8 +554,15 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
       p.a.flags[k] = p.a.flags[k] | kExpanded | (noise ? kChildF64 : 0);
     }
   }
+  // backup (MCTS_model.py:360) along the path k_select recorded
+  const int plen = p.g.path_len[g];
+  if (plen > 0) {
+    const int pn = lane < plen ? p.g.path[(int64_t)g * kMaxPath + lane] : 0;
+    backup_path(p, g, half, pn, plen - 1, v);
+  } else if (lane == 0) {
+    backup(p, g, half, leaf, v);
+  }
   if (lane == 0) {
-    backup(p, g, half, leaf, v);  // MCTS_model.py:360
     p.g.leaf[g] = -1;
     int sd = p.g.sims_done[g];
     if (!is_root) {  // the search-start root expansion is not one of the simulations
@@ -515,23 +585,18 @@ __device__ float root_pi(const Params& p, int g, int half, double temp, double u
   const int lane = lane_id();
   const int64_t r = nidx(p, half, g, 0);
   const int nc = p.a.nchild[r], fc = p.a.first[r];
-  // counts[a] = child visit count (float32), each lane finds the child for its square
+  const uint64_t lg = p.a.legal[r];
+  // counts[a] = child visit count (float32).  The children are every legal action in
+  // ascending order (or the single pass): lane j reads child j, lane a gathers from the
+  // lane holding its action's rank in the legal mask.
   float c = 0.0f, c64 = 0.0f;
   if (nc > 0) {
-    // children are sorted by action; lane j reads child j and scatters via shuffles
-    int act = 255;
     float cnt = 0.0f;
-    if (lane < nc) {
-      const int64_t ck = nidx(p, half, g, fc + lane);
-      act = p.a.action[ck];
-      cnt = (float)p.a.N[ck];
-    }
-    for (int j = 0; j < nc; ++j) {
-      const int aj = shfl(act, j);
-      const float cj = shfl(cnt, j);
-      if (aj == lane) c = cj;
-      if (aj == 64) c64 = cj;
-    }
+    if (lane < nc) cnt = (float)p.a.N[nidx(p, half, g, fc + lane)];
+    const int src = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
+    const float cj = shfl(cnt, src);
+    if (lg) c = ((lg >> lane) & 1) ? cj : 0.0f;
+    else c64 = cj;
   }
   float pi, p64;
   if (fabs(temp) < 1e-1) {
@@ -558,7 +623,6 @@ __device__ float root_pi(const Params& p, int g, int half, double temp, double u
     const float norm = np_sum65<float>(ce, ce64);
     if (norm < (float)1e-12) {
       // uniform over the root's valid actions (the children)
-      const uint64_t lg = p.a.legal[r];
       const float u = nc > 0 ? (float)(1.0 / (double)nc) : 0.0f;
       pi = (lg >> lane) & 1 ? u : 0.0f;
       p64 = lg == 0 ? u : 0.0f;
@@ -586,67 +650,103 @@ __device__ int sample_action(const float* pis, double u) {
   return idx > 64 ? 64 : idx;
 }
 
-// Re-root compaction: copy the subtree under old node `child` into the other arena half in
-// breadth-first order (children stay contiguous and ascending), making it node 0.  Whole
-// workgroup; map = LDS scratch of p.C ints (new index -> old index).
-__device__ int compact(const Params& p, int g, int child, int32_t* map) {
+// Re-root compaction: copy the subtree under old node `child` into the other arena half,
+// making it node 0.  Nodes keep their relative arena order (a stable stream compaction):
+// every node's parent and every sibling group's allocation precede its own, so `child` maps
+// to 0 and each sibling group -- allocated as one block -- stays contiguous and ascending,
+// which is all the descent relies on (the oracle's BFS order, oracle/mcts.py make_move,
+// yields the same tree).  Membership is found by pointer jumping on the parent links in LDS
+// instead of a level-by-level BFS: a handful of global round trips per re-root, not two per
+// tree level.  Whole workgroup; `scratch` = LDS of p.C ints, used as two u16 arrays (node
+// offsets from `child` are < p.C <= 32768, 0xffff = not in the subtree).
+__device__ int compact(const Params& p, int g, int child, int32_t* scratch) {
+  constexpr uint16_t kOut = 0xffff;
+  constexpr int kU = 8;  // parent loads in flight per thread
   __shared__ int s_scan[kMoveBlock / kWave];
+  uint16_t* rel = reinterpret_cast<uint16_t*>(scratch);  // old offset -> link, then new index
+  uint16_t* inv = rel + p.C;                             // new index -> old offset
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int oh = p.g.half[g], nh = oh ^ 1;
-  if (tid == 0) map[0] = child;
-  __syncthreads();
-  int lo = 0, hi = 1, n_new = 1;
-  while (lo < hi) {
-    for (int s0 = lo; s0 < hi; s0 += kMoveBlock) {
-      const int i = s0 + tid;
-      int old = -1, nc = 0;
-      if (i < hi) {
-        old = map[i];
-        const int64_t ok = nidx(p, oh, g, old);
-        if (p.a.flags[ok] & kExpanded) nc = p.a.nchild[ok];
-      }
-      // block exclusive scan of nc
-      int incl = nc;
+  const int span = p.g.n_nodes[g] - child;  // candidates: old nodes child .. n_nodes-1
+  // 1. rel[j] = parent of old node child+j as an offset from `child` (descendants of `child`
+  // all lie above it; a parent below it means "not in the subtree")
+  for (int j0 = 0; j0 < span; j0 += kMoveBlock * kU) {
+    int par[kU];
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) s_scan[wave] = incl;
-      __syncthreads();
-      int wbase = 0, tot = 0;
-      for (int w = 0; w < kMoveBlock / kWave; ++w) {
-        if (w < wave) wbase += s_scan[w];
-        tot += s_scan[w];
-      }
-      const int nfc = n_new + wbase + incl - nc;
-      if (i < hi) {
-        const int64_t ok = nidx(p, oh, g, old);
-        const int64_t nk = nidx(p, nh, g, i);
-        p.a.own[nk] = p.a.own[ok];
-        p.a.opp[nk] = p.a.opp[ok];
-        p.a.legal[nk] = p.a.legal[ok];
-        p.a.N[nk] = p.a.N[ok];
-        p.a.W[nk] = p.a.W[ok];
-        p.a.P[nk] = p.a.P[ok];
-        p.a.action[nk] = p.a.action[ok];
-        p.a.flags[nk] = p.a.flags[ok];
-        p.a.tval[nk] = p.a.tval[ok];
-        p.a.nchild[nk] = (uint8_t)nc;
-        p.a.first[nk] = nc ? nfc : -1;
-        if (i == 0) p.a.parent[nk] = -1;
-        const int ofc = p.a.first[ok];
-        for (int j = 0; j < nc; ++j) {
-          map[nfc + j] = ofc + j;
-          p.a.parent[nidx(p, nh, g, nfc + j)] = i;
-        }
-      }
-      n_new += tot;
-      __syncthreads();
+    for (int u = 0; u < kU; ++u) {
+      const int j = j0 + u * kMoveBlock + tid;
+      par[u] = (j > 0 && j < span) ? p.a.parent[nidx(p, oh, g, child + j)] : child;
     }
-    lo = hi;
-    hi = n_new;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int j = j0 + u * kMoveBlock + tid;
+      if (j < span) rel[j] = par[u] >= child ? (uint16_t)(par[u] - child) : kOut;
+    }
+  }
+  __syncthreads();
+  // 2. pointer jumping until every link is 0 (member) or kOut; in-place updates only ever
+  // replace a link by one of its ancestors' links
+  for (;;) {
+    int more = 0;
+    for (int j = tid; j < span; j += kMoveBlock) {
+      const uint16_t a = rel[j];
+      if (a != 0 && a != kOut) {
+        const uint16_t b = rel[a];
+        rel[j] = b;
+        more |= b != 0 && b != kOut;
+      }
+    }
+    if (!__syncthreads_or(more)) break;
+  }
+  // 3. new index = rank among members (block exclusive scan over contiguous thread ranges)
+  const int per = (span + kMoveBlock - 1) / kMoveBlock;
+  const int j0 = tid * per, j1 = min(j0 + per, span);
+  int cnt = 0;
+  for (int j = j0; j < j1; ++j) cnt += rel[j] == 0;
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off, kWave);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) s_scan[wave] = incl;
+  __syncthreads();
+  int base = 0, n_new = 0;
+  for (int w = 0; w < kMoveBlock / kWave; ++w) {
+    if (w < wave) base += s_scan[w];
+    n_new += s_scan[w];
+  }
+  int r = base + incl - cnt;
+  for (int j = j0; j < j1; ++j) {
+    if (rel[j] == 0) {
+      inv[r] = (uint16_t)j;
+      rel[j] = (uint16_t)r++;
+    } else {
+      rel[j] = kOut;
+    }
+  }
+  __syncthreads();
+  // 4. copy the members, translating parent / first-child links
+  for (int i = tid; i < n_new; i += kMoveBlock) {
+    const int j = inv[i];
+    const int64_t ok = nidx(p, oh, g, child + j);
+    const int64_t nk = nidx(p, nh, g, i);
+    const uint8_t f = p.a.flags[ok];
+    const bool ex = (f & kExpanded) != 0;
+    const int par = p.a.parent[ok], fc = p.a.first[ok];
+    p.a.own[nk] = p.a.own[ok];
+    p.a.opp[nk] = p.a.opp[ok];
+    p.a.legal[nk] = p.a.legal[ok];
+    p.a.N[nk] = p.a.N[ok];
+    p.a.W[nk] = p.a.W[ok];
+    p.a.P[nk] = p.a.P[ok];
+    p.a.action[nk] = p.a.action[ok];
+    p.a.flags[nk] = f;
+    p.a.tval[nk] = p.a.tval[ok];
+    p.a.nchild[nk] = ex ? p.a.nchild[ok] : (uint8_t)0;
+    p.a.first[nk] = ex ? (int)rel[fc - child] : -1;
+    p.a.parent[nk] = i == 0 ? -1 : (int)rel[par - child];
   }
   if (tid == 0) {
     p.g.half[g] = nh;
@@ -681,11 +781,23 @@ __device__ void new_game(const Params& p, int g) {
 }
 
 // get_training_data (self_play_worker.py:8-35) + append to the sample buffer.
-__device__ void finish_game(const Params& p, int g, int n_plies, int winner) {
+__device__ void finish_game(const Params& p, int g, int n_plies, int winner, int32_t* scratch) {
   __shared__ unsigned long long s_base;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
   const int64_t tb = (int64_t)g * p.T;
+  // the return chain below is sequential: stage its inputs in LDS with one parallel load
+  // (scratch = the caller's p.C-int LDS block) instead of two dependent loads per ply
+  double* s_vr = reinterpret_cast<double*>(scratch);
+  int8_t* s_pl = reinterpret_cast<int8_t*>(s_vr + n_plies);
+  const bool staged = n_plies * 9 <= p.C * 4;
+  if (staged) {
+    for (int t = tid; t < n_plies; t += blockDim.x) {
+      s_vr[t] = p.g.t_vroot[tb + t];
+      s_pl[t] = p.g.t_player[tb + t];
+    }
+    __syncthreads();
+  }
   if (tid == 0) {
     unsigned long long base = atomicAdd(&p.ctr->samples_n, (unsigned long long)n_plies);
     s_ok = (int64_t)(base + n_plies) <= p.s.cap;
@@ -698,14 +810,15 @@ __device__ void finish_game(const Params& p, int g, int n_plies, int winner) {
       double g_next = 0.0;
       int p_next = 0;
       for (int t = n_plies - 1; t >= 0; --t) {
-        const int pl = p.g.t_player[tb + t];
+        const int pl = staged ? s_pl[t] : p.g.t_player[tb + t];
         const double z = winner == 0 ? 0.0 : (pl == winner ? 1.0 : -1.0);
         double gt;
         if (t == n_plies - 1) {
           gt = z;
         } else {
           const double sign = pl == p_next ? 1.0 : -1.0;
-          gt = (1.0 - p.lambd) * p.g.t_vroot[tb + t] + p.lambd * sign * g_next;
+          const double vr = staged ? s_vr[t] : p.g.t_vroot[tb + t];
+          gt = (1.0 - p.lambd) * vr + p.lambd * sign * g_next;
         }
         p.s.z[base + t] = gt;
         g_next = gt;
@@ -722,8 +835,21 @@ __device__ void finish_game(const Params& p, int g, int n_plies, int winner) {
       p.s.player[base + t] = p.g.t_player[tb + t];
       p.s.slot[base + t] = g;
     }
-    for (int e = tid; e < n_plies * 65; e += blockDim.x)
-      p.s.pi[base * 65 + e] = p.g.t_pi[tb * 65 + e];
+    constexpr int kU = 8;  // loads in flight per thread
+    const int ne = n_plies * 65;
+    for (int e0 = 0; e0 < ne; e0 += kMoveBlock * kU) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + u * kMoveBlock + tid;
+        v[u] = e < ne ? p.g.t_pi[tb * 65 + e] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + u * kMoveBlock + tid;
+        if (e < ne) p.s.pi[base * 65 + e] = v[u];
+      }
+    }
   }
   __syncthreads();
 }
@@ -771,10 +897,18 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
         const double u = next_uniform(p, g, 0x2000u);
         const int a = sample_action(s_pi, u);
         // ---- the move: re-root to that child (MCTS.make_move, MCTS_model.py:200-215)
+        // the children are every legal action in ascending order (or the single pass):
+        // the chosen one's index follows from the root's legal mask, no per-child loads
         const int nc = p.a.nchild[r], fc = p.a.first[r];
+        const uint64_t lg = p.a.legal[r];
         int child = -1;
-        for (int j = 0; j < nc; ++j)
-          if (p.a.action[nidx(p, half, g, fc + j)] == a) child = fc + j;
+        if (nc > 0) {
+          if (lg) {
+            if (a < 64 && ((lg >> a) & 1)) child = fc + azb::popc(lg & ((1ull << a) - 1ull));
+          } else if (a == azb::kPass) {
+            child = fc;
+          }
+        }
         s_child = child;
         int term = 1, winner = 0;
         if (child >= 0) {
@@ -793,7 +927,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
     __syncthreads();
     if (s_term) {
       const int n_plies = ply + 1 < p.T ? ply + 1 : p.T;
-      finish_game(p, g, n_plies, s_winner);
+      finish_game(p, g, n_plies, s_winner, map);
       if (tid == 0) {
         p.g.winner[g] = s_winner;
         atomicAdd(&p.ctr->games_finished, 1ull);
@@ -1168,6 +1302,8 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.g.sims_done, G));
   chk(dalloc(e, &p.g.sims_target, G));
   chk(dalloc(e, &p.g.leaf, G));
+  chk(dalloc(e, &p.g.path, G * kMaxPath));
+  chk(dalloc(e, &p.g.path_len, G));
   chk(dalloc(e, &p.g.ply, G));
   chk(dalloc(e, &p.g.root_player, G));
   chk(dalloc(e, &p.g.winner, G));

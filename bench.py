@@ -60,6 +60,7 @@ HBM_COPY_GBS = 6290.0      # the guide's measured float4 copy rate (MI355X_MICRO
 STEP_BYTES = 43            # algorithmic bytes per board step
 MFMA16_PEAK = 2500.0       # dense bf16 / fp16 MFMA TFLOP/s (MI355X_MICROARCH.md)
 MFMA32_PEAK = 157.3        # dense fp32 MFMA TFLOP/s
+L2_PEAK_TBPS = 34.5        # aggregate L2 bandwidth, 8 XCDs x 4 MiB (MI355X_MICROARCH.md)
 DTYPE_LABEL = {
     "split3": "fp32-accurate net (trunk: fp32 operands split into 3 bf16 words, 6 bf16 MFMA "
               "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
@@ -180,11 +181,17 @@ def conv_roofline(sp, device, n_boards):
                 n_boards, C, 1, nat.stream_ptr()]
         kname, mult, peak = "k_conv3x3 (az_conv3x3_gpu, fp32 MFMA)", 1, MFMA32_PEAK
     else:
-        fn = nat.lib.az_conv3x3_mx_gpu
+        wino = getattr(conv, "algo", "direct") == "wino"
+        fn = nat.lib.az_conv3x3_wino_gpu if wino else nat.lib.az_conv3x3_mx_gpu
         args = [nat.ptr(x), nat.ptr(conv.wq), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y),
                 n_boards, C, 1, conv.mode, nat.stream_ptr()]
         mult = 6 if conv.precision == "split3" else 1
-        kname, peak = f"k_conv3x3_mx (az_conv3x3_mx_gpu, {conv.precision})", MFMA16_PEAK
+        if wino:  # 16 products per 2x2-output tile instead of 36: 256/576 of the direct MACs
+            mult = mult * 256 / 576
+            kname = f"k_conv3x3_wino (az_conv3x3_wino_gpu, Winograd F(2x2,3x3), {conv.precision})"
+        else:
+            kname = f"k_conv3x3_mx (az_conv3x3_mx_gpu, {conv.precision})"
+        peak = MFMA16_PEAK
     for _ in range(3):
         nat.check(fn(*args), kname)
     torch.cuda.synchronize()
@@ -198,12 +205,22 @@ def conv_roofline(sp, device, n_boards):
     ms = ev0.elapsed_time(ev1) / reps
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
-    return {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
-            "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None, "boards": n_boards,
-            "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
-            "mfma_flop_per_algorithmic_flop": mult,
-            "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1)}
+    out = {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
+           "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(achieved / peak, 4), "traffic": None, "boards": n_boards,
+           "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+           "mfma_flop_per_algorithmic_flop": round(mult, 4),
+           "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1)}
+    if conv.precision != "fp32":
+        # every workgroup streams the whole pre-split weight set from L2 (the bound measured
+        # for this kernel: scripts/exp/wino_exp.py)
+        per_wg = (16 if getattr(conv, "algo", "direct") == "wino" else 9) * C * C * \
+            (3 if conv.precision == "split3" else 1) * 2
+        wgs = (n_boards + 1) // 2 if getattr(conv, "algo", "direct") == "wino" else n_boards
+        out["l2_weight_stream"] = {"bytes_per_launch": per_wg * wgs,
+                                   "achieved_TBps": round(per_wg * wgs / (ms * 1e-3) / 1e12, 2),
+                                   "peak_TBps": L2_PEAK_TBPS}
+    return out
 
 
 def cpu_baseline(net, seconds):

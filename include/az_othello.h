@@ -300,6 +300,19 @@ int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w, const float
                            int32_t n_boards, int32_t channels, int32_t role, int32_t mode,
                            void* stream);
 
+/* The same convolution as Winograd F(2x2, 3x3) (csrc/conv_wino.hip): 2.25x fewer MFMA
+ * products; the input/output transforms only add and subtract and the weight transform
+ * G g G^T is done once in fp64, so SPLIT3 stays at the direct fp32 kernel's error (the
+ * test bar of az_conv3x3_mx_gpu).  wq: from az_conv3x3_wino_prep_gpu (w9 [9][Co][Ci] fp32
+ * -> [Ci/16][16 points][planes][Co][16] 16-bit words, 16*C*C*planes*2 bytes, 16-byte
+ * aligned).  Two boards per workgroup, 96 KiB LDS.  Same reference layers as
+ * az_conv3x3_gpu. */
+int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t mode,
+                             void* stream);
+int az_conv3x3_wino_gpu(const float* x, const void* wq, const float* bias, const float* res,
+                        float* y, int32_t n_boards, int32_t channels, int32_t relu,
+                        int32_t mode, void* stream);
+
 /* ---------------- replay buffer (device) -------------------------------------------
  * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with
  * equal (own, opp, version) — the reference's (sha1(canonical int8 board), version) —

@@ -47,6 +47,17 @@ def run(B, C):
         err = float((y.double() - ref).abs().max())
         ms = timed(lambda: nat.lib.az_conv3x3_mx_cfg_gpu(*args))
         out[name] = {"us": round(ms * 1e3, 1), "tf_equiv": round(fl / ms / 1e9, 1), "maxerr": err}
+    for name, mode in (("wino_split3", nat.AZ_CONV_SPLIT3), ("wino_fp16", nat.AZ_CONV_FP16)):
+        planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
+        wq = torch.empty(16 * C * C * planes, dtype=torch.int16, device="cuda")
+        nat.check(nat.lib.az_conv3x3_wino_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode, nat.stream_ptr()), "prep")
+        y = torch.empty_like(x)
+        args = [nat.ptr(x), nat.ptr(wq), nat.ptr(b), nat.ptr(r), nat.ptr(y), B, C, 1, mode,
+                nat.stream_ptr()]
+        nat.check(nat.lib.az_conv3x3_wino_gpu(*args), name); torch.cuda.synchronize()
+        err = float((y.double() - ref).abs().max())
+        ms = timed(lambda: nat.lib.az_conv3x3_wino_gpu(*args))
+        out[name] = {"us": round(ms * 1e3, 1), "tf_equiv": round(fl / ms / 1e9, 1), "maxerr": err}
     return out
 
 

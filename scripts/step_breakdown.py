@@ -12,7 +12,7 @@ import bench  # noqa: E402
 warm = int(sys.argv[1]) if len(sys.argv) > 1 else 30000
 torch.manual_seed(0)
 sp = BatchedSelfPlay(AlphaZeroNet(8, 65, 5, 128), bench.SELFPLAY_ARGS, 1024, seed=1)
-sp.reset(-1, 8000)
+sp.reset(-1, 401 * 60)
 blocks = []
 done = 0
 while done < warm:

@@ -67,8 +67,9 @@ def test_bias_act_kernel_matches_torch():
 
 
 @pytest.mark.parametrize("kind", ["az", "fast"])
-@pytest.mark.parametrize("conv,precision", [("hip", "split3"), ("hip", "fp32"), ("miopen", None)])
-def test_inference_copy_matches_module(kind, conv, precision):
+@pytest.mark.parametrize("conv,precision,algo", [("hip", "split3", "wino"), ("hip", "split3", "direct"),
+                                                 ("hip", "fp32", None), ("miopen", None, None)])
+def test_inference_copy_matches_module(kind, conv, precision, algo):
     torch.manual_seed(0)
     net = AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)
     # non-trivial BatchNorm statistics so the folding is exercised
@@ -79,7 +80,9 @@ def test_inference_copy_matches_module(kind, conv, precision):
             m.weight.data.uniform_(0.5, 1.5)
             m.bias.data.uniform_(-0.2, 0.2)
     net = net.cuda().eval()
-    fused = inference_copy(net, "cuda", conv=conv, precision=precision)
+    fused = inference_copy(net, "cuda", conv=conv, precision=precision, conv_algo=algo)
+    if algo is not None:
+        assert all(c.algo == algo for c in list(fused.c1) + list(fused.c2))
     x = torch.randint(-1, 2, (257, 64), device="cuda").float()
     with torch.no_grad():
         logits, v = net(x.view(-1, 1, 8, 8))
@@ -100,6 +103,22 @@ def _mx_conv(x, w, b, r, relu, mode):
     nat.check(nat.lib.az_conv3x3_mx_gpu(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
                                         None if r is None else nat.ptr(r), nat.ptr(y), x.shape[0],
                                         C, int(relu), mode, nat.stream_ptr()), "az_conv3x3_mx_gpu")
+    torch.cuda.synchronize()
+    return y
+
+
+def _wino_conv(x, w, b, r, relu, mode):
+    C = x.shape[1]
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
+    wq = torch.empty(16 * C * C * planes, dtype=torch.int16, device="cuda")
+    nat.check(nat.lib.az_conv3x3_wino_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode,
+                                               nat.stream_ptr()), "az_conv3x3_wino_prep_gpu")
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_wino_gpu(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
+                                          None if r is None else nat.ptr(r), nat.ptr(y),
+                                          x.shape[0], C, int(relu), mode, nat.stream_ptr()),
+              "az_conv3x3_wino_gpu")
     torch.cuda.synchronize()
     return y
 
@@ -141,6 +160,39 @@ def test_conv3x3_split3_is_fp32_accurate(C, B, res, relu):
 
 
 @pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("B", [1, 3, 130])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_conv3x3_winograd_is_fp32_accurate(C, B, res, relu):
+    """Winograd F(2x2,3x3) with split3 operands against fp64: the same bar as the direct
+    split3 kernel (max |err| <= 2x the fp32 kernel's + 1e-6, mean <= 2x), odd board counts
+    included (a workgroup holds two boards), and the fp32 tolerance against torch."""
+    x, w, b, r, ref64 = _case(C, B, C * 17 + B)
+    rr = r if res else None
+    y = _wino_conv(x, w, b, rr, relu, nat.AZ_CONV_SPLIT3)
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    y32 = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
+                                     nat.ptr(y32), B, C, int(relu), nat.stream_ptr()), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ref = ref64 + (r.cpu().double() if res else 0)
+    if relu:
+        ref = F.relu(ref)
+    e_w = (y.cpu().double() - ref).abs()
+    e_32 = (y32.cpu().double() - ref).abs()
+    assert e_w.max() <= 2 * e_32.max() + 1e-6, (e_w.max(), e_32.max())
+    assert e_w.mean() <= 2 * e_32.mean() + 1e-8, (e_w.mean(), e_32.mean())
+    torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+@pytest.mark.parametrize("C", [64, 128])
+def test_conv3x3_winograd_fp16_mode(C):
+    x, w, b, r, ref64 = _case(C, 37, C + 9)
+    y = _wino_conv(x, w, b, r, True, nat.AZ_CONV_FP16)
+    ref = F.relu(ref64 + r.cpu().double()).float().cuda()
+    torch.testing.assert_close(y, ref, atol=5e-3, rtol=5e-3)
+
+
+@pytest.mark.parametrize("C", [64, 128])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv3x3_fp16_mode(C, res):
     """fp16 inference (configs[4]): fp16 operands, fp32 accumulation; tolerance of fp16
@@ -174,7 +226,7 @@ def test_stem_fusion_is_bit_identical(kind, precision):
     same trunk output bit for bit as the stem kernel + plain convs."""
     torch.manual_seed(2)
     net = (AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)).cuda().eval()
-    fused = inference_copy(net, "cuda", precision=precision)
+    fused = inference_copy(net, "cuda", precision=precision, conv_algo="direct")
     x = torch.randint(-1, 2, (131, 1, 8, 8), device="cuda").float()
     with torch.no_grad():
         fused.fuse_stem = True
