@@ -32,7 +32,8 @@
 // experiment hooks (scripts/exp/wino_exp.py builds copies with bits set): 1 = no A reads in
 // the main loop, 2 = no weight loads in the main loop, 4 = no window loads / transform in
 // the main loop, 8 = no epilogue stores, 16 = workgroup 0 stamps s_memtime/s_memrealtime
-// around its main loop into y[0..3], 32 = no LDS barrier in the main loop.  Product: 0.
+// around its main loop into y[0..3], 32 = no LDS barrier in the main loop, 64 = no
+// residual loads.  Product: 0.
 #ifndef AZ_WN_EXP
 #define AZ_WN_EXP 0
 #endif
@@ -57,7 +58,7 @@ struct Wn {
   static constexpr int TPT = 256 / HALF;             // transform items per thread
   static constexpr int SLAB = 32 * 32;               // one (point, plane): 32 tiles x 16 ch x 2 B
   static constexpr int BUF = 16 * PLANES * SLAB;
-  static constexpr size_t XCH_BYTES = (size_t)CB * 2 * 16 * 2 * 64 * 4;  // epilogue exchange
+  static constexpr size_t XCH_BYTES = (size_t)CB * 2 * 8 * 2 * 64 * 8;  // epilogue exchange
   static constexpr size_t LDS_BYTES = 2 * BUF > XCH_BYTES ? 2 * BUF : XCH_BYTES;
   static constexpr int STEP_BYTES = PLANES * C * 32; // weight bytes per (chunk, point)
   static constexpr int QSTEPS = CHUNKS * 8;          // steps of one wave (8 points per chunk)
@@ -256,16 +257,20 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __rest
   }
 
   f32x2 raw[TPT][12], rw[TPT][8];
-  // ---- prologue: chunk 0 transformed into buffer 0, chunk 1's windows in flight, then the
-  // first kPd weight steps (the loop's vmcnt bookkeeping sees the same order on entry as
-  // around its back-edge: windows before weights)
-  wn_load_raw<G, 12>(raw, x, off, msk, 0, 0);
-  wn_rows<G>(rw, raw, msk, ph);
-  wn_load_raw<G, 12>(raw, x, off, msk, G::CHUNKS > 1 ? 1 : 0, 0);
-  __builtin_amdgcn_sched_barrier(0);
+  // ---- prologue: the windows of chunks 0 and 1 and the first kPd weight steps requested
+  // together (one round trip), chunk 0 transformed into buffer 0 (the loop's vmcnt
+  // bookkeeping sees the same order on entry as around its back-edge: windows before
+  // weights)
+  {
+    f32x2 raw0[TPT][12];
+    wn_load_raw<G, 12>(raw0, x, off, msk, 0, 0);
+    wn_load_raw<G, 12>(raw, x, off, msk, G::CHUNKS > 1 ? 1 : 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int i = 0; i < kPd; ++i) wn_load_b<G>(bf[i], wq_h, wlane, (i >> 3) * 16 + (i & 7));
-  __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < kPd; ++i) wn_load_b<G>(bf[i], wq_h, wlane, (i >> 3) * 16 + (i & 7));
+    __builtin_amdgcn_sched_barrier(0);
+    wn_rows<G>(rw, raw0, msk, ph);
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -331,68 +336,87 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __rest
   // sums over its 8 points (rows k of A^T M: half 0 holds M rows 0,1, half 1 rows 2,3),
   // hands the two outputs the other half finishes through LDS, and finishes its own two:
   // half 0 the tile's top outputs (2ty, 2tx + j), half 1 the bottom ones.
+  // Elements k and k+1 (adjacent tile rows of one board) travel together as f32x2, so the
+  // transform and epilogue arithmetic issues as packed VALU (no MFMAs to share issue with
+  // here) and the exchange as 8-byte LDS accesses.
   const int co = col0 + r;
   const float bv = bias[co];
-  float* xch = reinterpret_cast<float*>(lds);  // [cb][dest half][k][2][64 lanes]
-  float own[16][2];
-  lds_barrier();  // every wave is done reading the last A buffer
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    float m[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m[j] = acc_read(acc[j][k]);
-    // t0[l] = (A^T M)[0][l] partial, t1[l] = (A^T M)[1][l] partial
-    float t0[4], t1[4];
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      if (ph == 0) {
-        t0[l] = m[l] + m[4 + l];
-        t1[l] = m[4 + l];
-      } else {
-        t0[l] = m[l];
-        t1[l] = -m[l] - m[4 + l];
-      }
-    }
-    const float o0 = t0[0] + t0[1] + t0[2], o1 = t0[1] - t0[2] - t0[3];
-    const float o2 = t1[0] + t1[1] + t1[2], o3 = t1[1] - t1[2] - t1[3];
-    float* dst = xch + (((cb * 2 + (1 - ph)) * 16 + k) * 2) * 64 + lane;
-    dst[0] = ph == 0 ? o2 : o0;
-    dst[64] = ph == 0 ? o3 : o1;
-    own[k][0] = ph == 0 ? o0 : o2;
-    own[k][1] = ph == 0 ? o1 : o3;
-    __builtin_amdgcn_sched_barrier(0);  // one element's accumulators in VGPRs at a time
-  }
-  float rv[16][2];
-  if (RES) {  // every residual load in flight at once
+  f32x2 rv[8][2];
+  if (RES) {  // every residual load in flight before the transform arithmetic
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int T = (k & 3) + 8 * (k >> 2) + 4 * h;
       const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-      const bool in = bd < nb;
+      const bool in = bd < nb && !(AZ_WN_EXP & 64);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int pos = (2 * ty + ph) * 8 + 2 * tx + q;
-        rv[k][q] = in ? res[((size_t)(b0 + bd) * 64 + pos) * C + co] : 0.0f;
+        rv[k >> 1][q][k & 1] = in ? res[((size_t)(b0 + bd) * 64 + pos) * C + co] : 0.0f;
       }
     }
   }
-  lds_barrier();
-  const float* src = xch + ((cb * 2 + ph) * 16) * 2 * 64 + lane;
+  f32x2* xch = reinterpret_cast<f32x2*>(lds);  // [cb][dest half][k/2][2][64 lanes]
+  f32x2 own[8][2];
+  lds_barrier();  // every wave is done reading the last A buffer
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int T = (k & 3) + 8 * (k >> 2) + 4 * h;
-    const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-    if (bd >= nb) continue;  // uniform per k: rows of one k lie in one board
+  for (int kp = 0; kp < 8; ++kp) {
+    f32x2 m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      m[j] = f32x2{acc_read(acc[j][2 * kp]), acc_read(acc[j][2 * kp + 1])};
+    // t0[l] = (A^T M)[0][l] partial, t1[l] = (A^T M)[1][l] partial
+    f32x2 t0[4], t1[4];
+    if (ph == 0) {
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        t0[l] = m[l] + m[4 + l];
+        t1[l] = m[4 + l];
+      }
+    } else {
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        t0[l] = m[l];
+        t1[l] = -m[l] - m[4 + l];
+      }
+    }
+    const f32x2 o0 = t0[0] + t0[1] + t0[2], o1 = t0[1] - t0[2] - t0[3];
+    const f32x2 o2 = t1[0] + t1[1] + t1[2], o3 = t1[1] - t1[2] - t1[3];
+    f32x2* dst = xch + (((cb * 2 + (1 - ph)) * 8 + kp) * 2) * 64 + lane;
+    if (ph == 0) {
+      dst[0] = o2;
+      dst[64] = o3;
+      own[kp][0] = o0;
+      own[kp][1] = o1;
+    } else {
+      dst[0] = o0;
+      dst[64] = o1;
+      own[kp][0] = o2;
+      own[kp][1] = o3;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // two elements' accumulators in VGPRs at a time
+  }
+  lds_barrier();
+  const f32x2* src = xch + ((cb * 2 + ph) * 8) * 2 * 64 + lane;
+  const f32x2 bv2 = {bv, bv};
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    const int k0 = 2 * kp;
+    const int T0 = (k0 & 3) + 8 * (k0 >> 2) + 4 * h;  // tiles T0, T0 + 1: one board, one row
+    const int bd = T0 >> 4, ty = (T0 >> 2) & 3, tx = T0 & 3;
+    if (bd >= nb) continue;  // uniform per k pair
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int pos = (2 * ty + ph) * 8 + 2 * tx + q;
-      float v = own[k][q] + src[(k * 2 + q) * 64] + bv;
-      if (RES) v += rv[k][q];
-      if (RELU) v = fmaxf(v, 0.0f);
-      if (AZ_WN_EXP & 8) {
-        if (v == 12345.f) y[0] = v;
-      } else {
-        y[((size_t)(b0 + bd) * 64 + pos) * C + co] = v;
+      f32x2 v = own[kp][q] + src[(kp * 2 + q) * 64] + bv2;
+      if (RES) v += rv[kp][q];
+      if (RELU) v = __builtin_elementwise_max(v, f32x2{0.0f, 0.0f});
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int pos = (2 * ty + ph) * 8 + 2 * (tx + e) + q;
+        if (AZ_WN_EXP & 8) {
+          if (v[e] == 12345.f) y[0] = v[e];
+        } else {
+          y[((size_t)(b0 + bd) * 64 + pos) * C + co] = v[e];
+        }
       }
     }
   }
