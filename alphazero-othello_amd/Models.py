@@ -372,11 +372,47 @@ class FusedInferenceNet(nn.Module, Inference):
         self.c2 = nn.ModuleList([C3(b.conv2) for b in blocks])
 
     fuse_stem = True  # the stem evaluated inside the first block's convs (never stored)
+    # Winograd trunk as one launch (az_trunk_wino_gpu): bit-identical, but measured 3 % slower
+    # than the layer-by-layer graph at the bench batch (scripts/trunk_bench.py,
+    # profiles/r01_trunk_bench.jsonl), so off by default
+    fuse_trunk = False
+
+    def _trunk_kernel_ready(self):
+        """Whether the single-launch trunk (az_trunk_wino_gpu) applies: HIP stem and every
+        block conv on the Winograd kernel in one numerics mode."""
+        convs = list(self.c1) + list(self.c2)
+        if not (self.fuse_trunk and isinstance(self.stem, _HipStem) and convs):
+            return False
+        if not all(getattr(c, "algo", "") == "wino" and c.mode == convs[0].mode for c in convs):
+            return False
+        if not hasattr(self, "_tw"):
+            dev = self.stem.w9.device
+            order = [c for pair in zip(self.c1, self.c2) for c in pair]  # layer order
+            self._tw = {
+                "wq": torch.tensor([c.wq.data_ptr() for c in order], dtype=torch.int64, device=dev),
+                "bias": torch.tensor([c.bias.data_ptr() for c in order], dtype=torch.int64,
+                                     device=dev),
+                "mode": convs[0].mode, "C": convs[0].channels, "blocks": len(self.c1)}
+        return True
 
     def _trunk(self, x):
         if x.dim() == 3:
             x = x.unsqueeze(1)
         x = x.contiguous(memory_format=torch.channels_last)
+        if self._trunk_kernel_ready():
+            import az_native as nat
+
+            tw = self._tw
+            B = x.shape[0]
+            planes = x.reshape(B, 64).contiguous()
+            h = torch.empty((B, tw["C"], 8, 8), dtype=torch.float32, device=x.device,
+                            memory_format=torch.channels_last)
+            t = torch.empty_like(h, memory_format=torch.channels_last)
+            nat.check(nat.lib.az_trunk_wino_gpu(
+                nat.ptr(planes), nat.ptr(self.stem.w9), nat.ptr(self.stem.bias),
+                nat.ptr(tw["wq"]), nat.ptr(tw["bias"]), nat.ptr(h), nat.ptr(t), B,
+                tw["blocks"], tw["C"], tw["mode"], nat.stream_ptr()), "az_trunk_wino_gpu")
+            return h
         c1s, c2s = list(self.c1), list(self.c2)
         if (self.fuse_stem and isinstance(self.stem, _HipStem) and c1s
                 and getattr(c1s[0], "precision", "fp32") != "fp32"

@@ -58,7 +58,7 @@ struct Wn {
   static constexpr int TPT = 256 / HALF;             // transform items per thread
   static constexpr int SLAB = 32 * 32;               // one (point, plane): 32 tiles x 16 ch x 2 B
   static constexpr int BUF = 16 * PLANES * SLAB;
-  static constexpr size_t XCH_BYTES = (size_t)CB * 2 * 8 * 2 * 64 * 8;  // epilogue exchange
+  static constexpr size_t XCH_BYTES = (size_t)CB * 2 * 4 * 2 * 64 * 8;  // epilogue exchange
   static constexpr size_t LDS_BYTES = 2 * BUF > XCH_BYTES ? 2 * BUF : XCH_BYTES;
   static constexpr int STEP_BYTES = PLANES * C * 32; // weight bytes per (chunk, point)
   static constexpr int QSTEPS = CHUNKS * 8;          // steps of one wave (8 points per chunk)
@@ -206,18 +206,20 @@ __device__ __forceinline__ void wn_sched() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// One conv layer for board pair `pair` (boards 2*pair, 2*pair+1) by the whole workgroup;
+// `lds` = G::LDS_BYTES of LDS.  Ends with a workgroup barrier: its outputs are visible to
+// the workgroup and its LDS is free again.
 template <class G, bool RES, bool RELU>
-__global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __restrict__ x,
-                                                             const char* __restrict__ wq,
-                                                             const float* __restrict__ bias,
-                                                             const float* __restrict__ res,
-                                                             float* __restrict__ y,
-                                                             int n_boards) {
+__device__ __forceinline__ void wino_pair(const float* __restrict__ x, const char* __restrict__ wq,
+                                          const float* __restrict__ bias,
+                                          const float* res, float* y,  // may alias (in place)
+                                          int n_boards, int pair, char* lds) {
   constexpr int C = G::C, TPT = G::TPT;
   const uint64_t rt_entry = (AZ_WN_EXP & 16) ? __builtin_amdgcn_s_memrealtime() : 0;
-  extern __shared__ float4 lds4[];
-  char* lds = reinterpret_cast<char*>(lds4);
-  const int tid = threadIdx.x;
+  // laundered: nothing lane-dependent is hoisted out of a caller's layer loop (it would sit
+  // in registers across every layer and spill)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   // wave = (point half ph, column block cb): points 8ph..8ph+7, columns 32cb..32cb+31.
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __rest
   const int ph = __builtin_amdgcn_readfirstlane(wave / G::CB);
   const int cb = __builtin_amdgcn_readfirstlane(wave % G::CB);
   const int col0 = cb * 32;
-  const int b0 = blockIdx.x * 2;
+  const int b0 = pair * 2;
   const int nb = n_boards - b0 < 2 ? n_boards - b0 : 2;
   constexpr int qlast = G::QSTEPS - 1;
   constexpr int kRing = 4, kPd = 3;  // weight ring and prefetch distance (steps)
@@ -339,93 +341,174 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __rest
   // Elements k and k+1 (adjacent tile rows of one board) travel together as f32x2, so the
   // transform and epilogue arithmetic issues as packed VALU (no MFMAs to share issue with
   // here) and the exchange as 8-byte LDS accesses.
+  // Two rounds of 4 element pairs bound the registers (residuals, own partials).
   const int co = col0 + r;
   const float bv = bias[co];
-  f32x2 rv[8][2];
-  if (RES) {  // every residual load in flight before the transform arithmetic
+  const f32x2 bv2 = {bv, bv};
+  f32x2* xch = reinterpret_cast<f32x2*>(lds);  // [cb][dest half][k/2 of the round][2][64]
+  constexpr int kR = 4;                         // element pairs per round
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int T = (k & 3) + 8 * (k >> 2) + 4 * h;
-      const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-      const bool in = bd < nb && !(AZ_WN_EXP & 64);
+  for (int r0 = 0; r0 < 8; r0 += kR) {
+    f32x2 rv[kR][2];
+    if (RES) {  // the round's residual loads in flight before its transform arithmetic
+#pragma unroll
+      for (int i = 0; i < 2 * kR; ++i) {
+        const int k = 2 * r0 + i;
+        const int T = (k & 3) + 8 * (k >> 2) + 4 * h;
+        const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
+        const bool in = bd < nb && !(AZ_WN_EXP & 64);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int pos = (2 * ty + ph) * 8 + 2 * tx + q;
+          rv[i >> 1][q][i & 1] = in ? res[((size_t)(b0 + bd) * 64 + pos) * C + co] : 0.0f;
+        }
+      }
+    }
+    f32x2 own[kR][2];
+    // every wave is done reading the last A buffer (round 0) / the previous round's exchange
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < kR; ++i) {
+      const int kp = r0 + i;
+      f32x2 m[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        m[j] = f32x2{acc_read(acc[j][2 * kp]), acc_read(acc[j][2 * kp + 1])};
+      // t0[l] = (A^T M)[0][l] partial, t1[l] = (A^T M)[1][l] partial
+      f32x2 t0[4], t1[4];
+      if (ph == 0) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          t0[l] = m[l] + m[4 + l];
+          t1[l] = m[4 + l];
+        }
+      } else {
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          t0[l] = m[l];
+          t1[l] = -m[l] - m[4 + l];
+        }
+      }
+      const f32x2 o0 = t0[0] + t0[1] + t0[2], o1 = t0[1] - t0[2] - t0[3];
+      const f32x2 o2 = t1[0] + t1[1] + t1[2], o3 = t1[1] - t1[2] - t1[3];
+      f32x2* dst = xch + (((cb * 2 + (1 - ph)) * kR + i) * 2) * 64 + lane;
+      if (ph == 0) {
+        dst[0] = o2;
+        dst[64] = o3;
+        own[i][0] = o0;
+        own[i][1] = o1;
+      } else {
+        dst[0] = o0;
+        dst[64] = o1;
+        own[i][0] = o2;
+        own[i][1] = o3;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // two elements' accumulators in VGPRs at a time
+    }
+    lds_barrier();
+    const f32x2* src = xch + ((cb * 2 + ph) * kR) * 2 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < kR; ++i) {
+      const int k0 = 2 * (r0 + i);
+      const int T0 = (k0 & 3) + 8 * (k0 >> 2) + 4 * h;  // tiles T0, T0 + 1: one board, one row
+      const int bd = T0 >> 4, ty = (T0 >> 2) & 3, tx = T0 & 3;
+      if (bd >= nb) continue;  // uniform per k pair
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int pos = (2 * ty + ph) * 8 + 2 * tx + q;
-        rv[k >> 1][q][k & 1] = in ? res[((size_t)(b0 + bd) * 64 + pos) * C + co] : 0.0f;
-      }
-    }
-  }
-  f32x2* xch = reinterpret_cast<f32x2*>(lds);  // [cb][dest half][k/2][2][64 lanes]
-  f32x2 own[8][2];
-  lds_barrier();  // every wave is done reading the last A buffer
+        f32x2 v = own[i][q] + src[(i * 2 + q) * 64] + bv2;
+        if (RES) v += rv[i][q];
+        if (RELU) v = __builtin_elementwise_max(v, f32x2{0.0f, 0.0f});
 #pragma unroll
-  for (int kp = 0; kp < 8; ++kp) {
-    f32x2 m[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      m[j] = f32x2{acc_read(acc[j][2 * kp]), acc_read(acc[j][2 * kp + 1])};
-    // t0[l] = (A^T M)[0][l] partial, t1[l] = (A^T M)[1][l] partial
-    f32x2 t0[4], t1[4];
-    if (ph == 0) {
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        t0[l] = m[l] + m[4 + l];
-        t1[l] = m[4 + l];
-      }
-    } else {
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        t0[l] = m[l];
-        t1[l] = -m[l] - m[4 + l];
-      }
-    }
-    const f32x2 o0 = t0[0] + t0[1] + t0[2], o1 = t0[1] - t0[2] - t0[3];
-    const f32x2 o2 = t1[0] + t1[1] + t1[2], o3 = t1[1] - t1[2] - t1[3];
-    f32x2* dst = xch + (((cb * 2 + (1 - ph)) * 8 + kp) * 2) * 64 + lane;
-    if (ph == 0) {
-      dst[0] = o2;
-      dst[64] = o3;
-      own[kp][0] = o0;
-      own[kp][1] = o1;
-    } else {
-      dst[0] = o0;
-      dst[64] = o1;
-      own[kp][0] = o2;
-      own[kp][1] = o3;
-    }
-    __builtin_amdgcn_sched_barrier(0);  // two elements' accumulators in VGPRs at a time
-  }
-  lds_barrier();
-  const f32x2* src = xch + ((cb * 2 + ph) * 8) * 2 * 64 + lane;
-  const f32x2 bv2 = {bv, bv};
-#pragma unroll
-  for (int kp = 0; kp < 8; ++kp) {
-    const int k0 = 2 * kp;
-    const int T0 = (k0 & 3) + 8 * (k0 >> 2) + 4 * h;  // tiles T0, T0 + 1: one board, one row
-    const int bd = T0 >> 4, ty = (T0 >> 2) & 3, tx = T0 & 3;
-    if (bd >= nb) continue;  // uniform per k pair
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      f32x2 v = own[kp][q] + src[(kp * 2 + q) * 64] + bv2;
-      if (RES) v += rv[kp][q];
-      if (RELU) v = __builtin_elementwise_max(v, f32x2{0.0f, 0.0f});
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int pos = (2 * ty + ph) * 8 + 2 * (tx + e) + q;
-        if (AZ_WN_EXP & 8) {
-          if (v[e] == 12345.f) y[0] = v[e];
-        } else {
-          y[((size_t)(b0 + bd) * 64 + pos) * C + co] = v[e];
+        for (int e = 0; e < 2; ++e) {
+          const int pos = (2 * ty + ph) * 8 + 2 * (tx + e) + q;
+          if (AZ_WN_EXP & 8) {
+            if (v[e] == 12345.f) y[0] = v[e];
+          } else {
+            y[((size_t)(b0 + bd) * 64 + pos) * C + co] = v[e];
+          }
         }
       }
     }
   }
   if ((AZ_WN_EXP & 16) && tid == 0) {  // per-workgroup timeline (entry, loop start/end, end)
-    uint64_t* t = reinterpret_cast<uint64_t*>(y) + 4 + 4 * blockIdx.x;
+    uint64_t* t = reinterpret_cast<uint64_t*>(y) + 4 + 4 * pair;
     t[0] = rt_entry;
     t[1] = rt0;
     t[2] = rt1;
     t[3] = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+}
+
+template <class G, bool RES, bool RELU>
+__global__ __launch_bounds__(G::THREADS) void k_conv3x3_wino(const float* __restrict__ x,
+                                                             const char* __restrict__ wq,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ res,
+                                                             float* __restrict__ y,
+                                                             int n_boards) {
+  extern __shared__ float4 lds4[];
+  wino_pair<G, RES, RELU>(x, wq, bias, res, y, n_boards, blockIdx.x, reinterpret_cast<char*>(lds4));
+}
+
+// The whole residual trunk in one launch: stem (1 -> C 3x3 conv + bias + ReLU, k_conv_stem's
+// fmaf chain) then n_blocks residual blocks (conv + ReLU, conv + residual + ReLU), every
+// layer by the same code as k_conv3x3_wino, so the result is bit-identical to the
+// layer-by-layer launches.  A convolution only mixes positions within a board, so each
+// workgroup carries its board pairs through every layer without a grid-wide barrier: no
+// launch gaps, and each layer reads its input from this CU's recent writes (L2) instead of
+// a previous kernel's.  Workgroups walk pairs blockIdx.x, +gridDim.x, ...
+struct TrunkArgs {
+  const float* planes;        // [n][64] canonical boards
+  const float* stem_w;        // [9][C]
+  const float* stem_b;        // [C]
+  const char* const* wq;      // [2 * n_blocks] per-conv Winograd weights (prep layout)
+  const float* const* bias;   // [2 * n_blocks]
+  float* h;                   // [n][64][C]: the stem output, then each block's output
+  float* t;                   // [n][64][C]: each block's first conv output
+  int n_boards, n_blocks;
+};
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS) void k_trunk_wino(TrunkArgs a) {
+  constexpr int C = G::C;
+  extern __shared__ float4 lds4[];
+  char* lds = reinterpret_cast<char*>(lds4);
+  const int npairs = (a.n_boards + 1) / 2;
+  for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+    // stem of the pair's boards (float4 of channels per item, k_conv_stem's tap order)
+    const int nb = a.n_boards - 2 * p < 2 ? a.n_boards - 2 * p : 2;
+    for (int i = threadIdx.x; i < nb * 64 * (C / 4); i += G::THREADS) {
+      const int pos = i / (C / 4), co = (i % (C / 4)) * 4;
+      const int b = 2 * p + (pos >> 6), q = pos & 63, py = q >> 3, px = q & 7;
+      const float* in = a.planes + (size_t)b * 64;
+      float4 acc = *reinterpret_cast<const float4*>(a.stem_b + co);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const int yy = py + tp / 3 - 1, xx = px + tp % 3 - 1;
+        if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
+          const float v = in[yy * 8 + xx];
+          const float4 wv = *reinterpret_cast<const float4*>(a.stem_w + tp * C + co);
+          acc.x = fmaf(v, wv.x, acc.x);
+          acc.y = fmaf(v, wv.y, acc.y);
+          acc.z = fmaf(v, wv.z, acc.z);
+          acc.w = fmaf(v, wv.w, acc.w);
+        }
+      }
+      acc.x = fmaxf(acc.x, 0.f);
+      acc.y = fmaxf(acc.y, 0.f);
+      acc.z = fmaxf(acc.z, 0.f);
+      acc.w = fmaxf(acc.w, 0.f);
+      reinterpret_cast<float4*>(a.h + ((size_t)b * 64 + q) * C)[co / 4] = acc;
+    }
+    __syncthreads();
+    for (int blk = 0; blk < a.n_blocks; ++blk) {
+      wino_pair<G, false, true>(a.h, a.wq[2 * blk], a.bias[2 * blk], nullptr, a.t, a.n_boards, p,
+                                lds);
+      // in place: each output element's residual is read by the lane that then writes it
+      wino_pair<G, true, true>(a.t, a.wq[2 * blk + 1], a.bias[2 * blk + 1], a.h, a.h,
+                               a.n_boards, p, lds);
+    }
   }
 }
 
@@ -505,6 +588,52 @@ int launch_wino(const float* x, const void* wq, const float* bias, const float* 
 }
 
 }  // namespace
+
+namespace {
+template <class G>
+int launch_trunk(const TrunkArgs& a, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino<G>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    AZ_HIP(hipGetDevice(&dev));
+    AZ_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n_cu <= 0) n_cu = 256;
+  }
+  const int pairs = (a.n_boards + 1) / 2;
+  // one workgroup per CU (its LDS and registers allow no second), pairs dealt round robin
+  const unsigned grid = (unsigned)(pairs < n_cu ? pairs : n_cu);
+  hipLaunchKernelGGL(k_trunk_wino<G>, dim3(grid), dim3(G::THREADS), G::LDS_BYTES, s, a);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+}  // namespace
+
+extern "C" int az_trunk_wino_gpu(const float* planes, const float* stem_w, const float* stem_b,
+                                 const void* const* wq, const float* const* bias, float* h,
+                                 float* t, int32_t n_boards, int32_t n_blocks, int32_t channels,
+                                 int32_t mode, void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && n_blocks >= 0, AZ_ERR_ARG, "az_trunk_wino_gpu: negative size");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(planes && stem_w && stem_b && h && t && h != t && (n_blocks == 0 || (wq && bias)),
+             AZ_ERR_ARG, "az_trunk_wino_gpu: null or aliased buffer");
+  AZ_REQUIRE(((uintptr_t)stem_w | (uintptr_t)stem_b | (uintptr_t)h | (uintptr_t)t) % 16 == 0,
+             AZ_ERR_ARG, "az_trunk_wino_gpu: buffers must be 16-byte aligned");
+  const TrunkArgs a{planes, stem_w, stem_b, reinterpret_cast<const char* const*>(wq), bias, h, t,
+                    n_boards, n_blocks};
+  hipStream_t s = azc::as_stream(stream);
+  if (channels == 128 && mode == AZ_CONV_SPLIT3) return launch_trunk<Wn<128, AZ_CONV_SPLIT3>>(a, s);
+  if (channels == 64 && mode == AZ_CONV_SPLIT3) return launch_trunk<Wn<64, AZ_CONV_SPLIT3>>(a, s);
+  if (channels == 128 && mode == AZ_CONV_FP16) return launch_trunk<Wn<128, AZ_CONV_FP16>>(a, s);
+  if (channels == 64 && mode == AZ_CONV_FP16) return launch_trunk<Wn<64, AZ_CONV_FP16>>(a, s);
+  return azc::set_error(AZ_ERR_ARG, "az_trunk_wino_gpu: channels %d / mode %d unsupported",
+                        channels, mode);
+}
 
 extern "C" int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t channels,
                                         int32_t mode, void* stream) {

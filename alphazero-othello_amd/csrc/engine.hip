@@ -27,6 +27,7 @@
 // reference's NumPy-2 (NEP 50) promotion; the library is built with -ffp-contract=off.
 #include <math.h>
 
+#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -1422,7 +1423,11 @@ int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
   // call; cap them per step so one end-game tree (every simulation terminal) cannot hold
   // the whole batched step for hundreds of dependent descents.  Host-driven engines step
   // one search at a time and take them all at once.
-  const int max_descents = e->p.auto_play ? 4 : 4 * (e->p.sims + 1) + 64;
+  static const int env_md = [] {
+    const char* v = getenv("AZ_MAX_DESCENTS");  // experiment knob (scripts/exp), default 4
+    return v ? atoi(v) : 0;
+  }();
+  const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4) : 4 * (e->p.sims + 1) + 64;
   hipLaunchKernelGGL(k_select, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in, leaf_o,
                      max_descents);
   AZ_HIP(hipGetLastError());

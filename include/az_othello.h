@@ -313,6 +313,22 @@ int az_conv3x3_wino_gpu(const float* x, const void* wq, const float* bias, const
                         float* y, int32_t n_boards, int32_t channels, int32_t relu,
                         int32_t mode, void* stream);
 
+/* The whole residual trunk of AlphaZeroNet / FastOthelloNet in one launch
+ * (csrc/conv_wino.hip): the stem (az_conv_stem_gpu's arithmetic) then n_blocks residual
+ * blocks of two Winograd convolutions (az_conv3x3_wino_gpu's arithmetic: conv + ReLU, conv +
+ * residual + ReLU), bit-identical to those launches one layer at a time.  Each workgroup
+ * carries whole board pairs through every layer (a conv mixes positions within a board
+ * only), so no grid-wide barrier is needed.  planes float [n][64]; stem_w [9][C]; stem_b
+ * [C]; wq / bias: device arrays of 2*n_blocks device pointers (az_conv3x3_wino_prep_gpu
+ * weights, fp32 biases) in layer order; h [n][64][C] receives the trunk output (NHWC), t
+ * [n][64][C] is scratch.  Replaces reference Models.py:209-210 (relu(bn0(conv0)) and the res
+ * tower, AlphaZeroNet.forward) / :147-148 (initial_conv + res_block, the FastOthelloNet
+ * forward). */
+int az_trunk_wino_gpu(const float* planes, const float* stem_w, const float* stem_b,
+                      const void* const* wq, const float* const* bias, float* h, float* t,
+                      int32_t n_boards, int32_t n_blocks, int32_t channels, int32_t mode,
+                      void* stream);
+
 /* ---------------- replay buffer (device) -------------------------------------------
  * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with
  * equal (own, opp, version) — the reference's (sha1(canonical int8 board), version) —

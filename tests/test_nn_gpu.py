@@ -235,3 +235,22 @@ def test_stem_fusion_is_bit_identical(kind, precision):
         b = fused._trunk(x)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["az", "fast"])
+def test_trunk_kernel_is_bit_identical(kind):
+    """az_trunk_wino_gpu (stem + every residual block in one launch, board pairs carried
+    through all layers by one workgroup) gives the layer-by-layer launches' trunk output bit
+    for bit, odd board count included."""
+    torch.manual_seed(3)
+    net = (AlphaZeroNet(8, 65, 5, 128) if kind == "az" else FastOthelloNet(8, 65)).cuda().eval()
+    fused = inference_copy(net, "cuda", precision="split3", conv_algo="wino")
+    x = torch.randint(-1, 2, (301, 1, 8, 8), device="cuda").float()
+    with torch.no_grad():
+        fused.fuse_trunk = True
+        assert fused._trunk_kernel_ready()
+        a = fused._trunk(x)
+        fused.fuse_trunk = False
+        b = fused._trunk(x)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
