@@ -181,38 +181,50 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3(const float* __restrict_
   }
 }
 
-// Stem: Ci = 1 (the canonical board plane), 9 taps; one thread per (position, 4 channels).
+// Stem: Ci = 1 (the canonical board plane), 9 taps.  One board per workgroup: its 64 plane values in LDS, each thread's 4 channels' 9 tap
+// weights in registers, 8 positions per thread; a wave stores two whole 512-byte position
+// rows per instruction.  Same tap order and fmaf chain per output as every other stem
+// evaluation (az_conv3x3_mx_stem_gpu relies on bit-identity).
 template <int CO>
 __global__ __launch_bounds__(256) void k_conv_stem(const float* __restrict__ planes,
                                                    const float* __restrict__ w,
                                                    const float* __restrict__ bias,
-                                                   float* __restrict__ y, int64_t n_out4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_out4;
-       i += (int64_t)gridDim.x * 256) {
-    const int64_t pos = i / (CO / 4);
-    const int co = (int)(i % (CO / 4)) * 4;
-    const int64_t b = pos >> 6;
-    const int p = (int)(pos & 63), py = p >> 3, px = p & 7;
-    const float* in = planes + b * 64;
-    float4 acc = *reinterpret_cast<const float4*>(bias + co);
-    // same tap order as the MFMA path (tap-major); one fma chain per output
+                                                   float* __restrict__ y, int64_t n_boards) {
+  constexpr int G4 = CO / 4;            // float4 channel groups per position
+  constexpr int PPI = 256 / G4;         // positions per pass of the workgroup
+  __shared__ float s_pl[64];
+  const int tid = threadIdx.x;
+  const int co = (tid % G4) * 4;
+  float4 wv[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
-      if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
-        const float v = in[yy * 8 + xx];
-        const float4 wv = *reinterpret_cast<const float4*>(w + t * CO + co);
-        acc.x = fmaf(v, wv.x, acc.x);
-        acc.y = fmaf(v, wv.y, acc.y);
-        acc.z = fmaf(v, wv.z, acc.z);
-        acc.w = fmaf(v, wv.w, acc.w);
+  for (int t = 0; t < 9; ++t) wv[t] = *reinterpret_cast<const float4*>(w + t * CO + co);
+  const float4 bv = *reinterpret_cast<const float4*>(bias + co);
+  for (int64_t b = blockIdx.x; b < n_boards; b += gridDim.x) {
+    __syncthreads();  // the previous board's planes are no longer read
+    if (tid < 64) s_pl[tid] = planes[b * 64 + tid];
+    __syncthreads();
+    float4* out = reinterpret_cast<float4*>(y + b * 64 * CO);
+#pragma unroll
+    for (int p0 = 0; p0 < 64; p0 += PPI) {
+      const int p = p0 + tid / G4, py = p >> 3, px = p & 7;
+      float4 acc = bv;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+        if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
+          const float v = s_pl[yy * 8 + xx];
+          acc.x = fmaf(v, wv[t].x, acc.x);
+          acc.y = fmaf(v, wv[t].y, acc.y);
+          acc.z = fmaf(v, wv[t].z, acc.z);
+          acc.w = fmaf(v, wv[t].w, acc.w);
+        }
       }
+      acc.x = fmaxf(acc.x, 0.f);
+      acc.y = fmaxf(acc.y, 0.f);
+      acc.z = fmaxf(acc.z, 0.f);
+      acc.w = fmaxf(acc.w, 0.f);
+      out[p * G4 + co / 4] = acc;
     }
-    acc.x = fmaxf(acc.x, 0.f);
-    acc.y = fmaxf(acc.y, 0.f);
-    acc.z = fmaxf(acc.z, 0.f);
-    acc.w = fmaxf(acc.w, 0.f);
-    reinterpret_cast<float4*>(y)[i] = acc;
   }
 }
 
@@ -308,15 +320,13 @@ extern "C" int az_conv_stem_gpu(const float* planes, const float* w9, const floa
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(planes && w9 && bias && y, AZ_ERR_ARG, "az_conv_stem_gpu: null buffer");
   hipStream_t s = azc::as_stream(stream);
-  const int64_t n4 = (int64_t)n_boards * 64 * channels / 4;
-  int64_t blocks = (n4 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  const int64_t blocks = n_boards < 8192 ? n_boards : 8192;  // one board per workgroup pass
   if (channels == 128)
     hipLaunchKernelGGL(k_conv_stem<128>, dim3((unsigned)blocks), dim3(256), 0, s, planes, w9,
-                       bias, y, n4);
+                       bias, y, (int64_t)n_boards);
   else if (channels == 64)
     hipLaunchKernelGGL(k_conv_stem<64>, dim3((unsigned)blocks), dim3(256), 0, s, planes, w9,
-                       bias, y, n4);
+                       bias, y, (int64_t)n_boards);
   else
     return azc::set_error(AZ_ERR_ARG, "az_conv_stem_gpu: channels must be 64 or 128");
   AZ_HIP(hipGetLastError());
