@@ -15,7 +15,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libaz_othello.so")
+# AZ_LIB_PATH: an alternative build of the same library (experiment builds, scripts/exp)
+LIB_PATH = os.environ.get("AZ_LIB_PATH") or os.path.join(HERE, "libaz_othello.so")
 
 AZ_OK = 0
 AZ_ERR_ILLEGAL = -1

@@ -84,12 +84,23 @@ AZ_HD uint64_t rev64(uint64_t x) {
 // Whole-word shifts by a constant.  On the device they are pinned to one v_lshlrev_b64 /
 // v_lshrrev_b64 on a register pair: left to itself the compiler narrows a 64-bit shift
 // whose halves feed bop3 into two or three 32-bit ops.
+#ifndef AZ_SHIFT_ASM
+#define AZ_SHIFT_ASM 1  // measured faster than the alignbit pairs (0.171 vs 0.200 ms / 2^24)
+#endif
 template <int S>
 AZ_HD uint64_t shl(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(S > 0 && S < 32, "constant shifts below one word");
+#if AZ_SHIFT_ASM
   uint64_t r;
   asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
   return r;
+#else
+  // two 32-bit ops (v_lshlrev_b32 + v_alignbit_b32), no inline asm (after which the hazard
+  // recognizer pads an s_nop); slower here: the 64-bit shift is one full-rate instruction
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, 32 - S) << 32) | (uint32_t)(lo << S);
+#endif
 #else
   return x << S;
 #endif
@@ -97,11 +108,30 @@ AZ_HD uint64_t shl(uint64_t x) {
 template <int S>
 AZ_HD uint64_t shr(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(S > 0 && S < 32, "constant shifts below one word");
+#if AZ_SHIFT_ASM
   uint64_t r;
   asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
   return r;
 #else
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> S) << 32) | __builtin_amdgcn_alignbit(hi, lo, S);
+#endif
+#else
   return x >> S;
+#endif
+}
+
+// a << S and b >> S in one asm statement: the hazard recognizer pads one s_nop after an
+// inline-asm block it cannot see into, so pairing the fill's two directions halves them
+template <int S>
+AZ_HD void shl_shr(uint64_t a, uint64_t b, uint64_t& l, uint64_t& r) {
+#if defined(__HIP_DEVICE_COMPILE__) && AZ_SHIFT_ASM
+  asm("v_lshlrev_b64 %0, %2, %3\n\tv_lshrrev_b64 %1, %2, %4"
+      : "=&v"(l), "=v"(r) : "i"(S), "v"(a), "v"(b));
+#else
+  l = shl<S>(a);
+  r = shr<S>(b);
 #endif
 }
 
@@ -110,17 +140,23 @@ AZ_HD uint64_t shr(uint64_t x) {
 template <int D>
 AZ_HD uint64_t moves_dir(uint64_t P, uint64_t M) {
   using namespace tt;
-  uint64_t fl = M & shl<D>(P);
-  uint64_t fr = M & shr<D>(P);
-  fl = bop3<A | (B & C)>(fl, M, shl<D>(fl));
-  fr = bop3<A | (B & C)>(fr, M, shr<D>(fr));
+  uint64_t sl, sr;
+  shl_shr<D>(P, P, sl, sr);
+  uint64_t fl = M & sl;
+  uint64_t fr = M & sr;
+  shl_shr<D>(fl, fr, sl, sr);
+  fl = bop3<A | (B & C)>(fl, M, sl);
+  fr = bop3<A | (B & C)>(fr, M, sr);
   const uint64_t ml = M & shl<D>(M);
   const uint64_t mr = shr<D>(ml);
-  fl = bop3<A | (B & C)>(fl, ml, shl<2 * D>(fl));
-  fr = bop3<A | (B & C)>(fr, mr, shr<2 * D>(fr));
-  fl = bop3<A | (B & C)>(fl, ml, shl<2 * D>(fl));
-  fr = bop3<A | (B & C)>(fr, mr, shr<2 * D>(fr));
-  return shl<D>(fl) | shr<D>(fr);
+  shl_shr<2 * D>(fl, fr, sl, sr);
+  fl = bop3<A | (B & C)>(fl, ml, sl);
+  fr = bop3<A | (B & C)>(fr, mr, sr);
+  shl_shr<2 * D>(fl, fr, sl, sr);
+  fl = bop3<A | (B & C)>(fl, ml, sl);
+  fr = bop3<A | (B & C)>(fr, mr, sr);
+  shl_shr<D>(fl, fr, sl, sr);
+  return sl | sr;
 }
 
 // Horizontal moves by carry propagation: a run of opponent stones (columns 1..6, so no
