@@ -315,15 +315,17 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   const int lane = lane_id();
+  // every per-slot word in one round trip
   const int status = p.g.status[g];
   const unsigned long long step = p.ctr->step;
-  if (status != kActive || (long long)step < (long long)p.g.start_step[g]) {
-    emit_none(nn_in, leaf_o, g);
-    return;
-  }
+  const int start_step = p.g.start_step[g];
   const int half = p.g.half[g];
   int sims_done = p.g.sims_done[g];
   const int target = p.g.sims_target[g];
+  if (status != kActive || (long long)step < (long long)start_step) {
+    emit_none(nn_in, leaf_o, g);
+    return;
+  }
   int leaf = -1;
   int depth = 0;      // depth of the current node
   int path_node = 0;  // lane d: node at depth d of the current descent
@@ -433,12 +435,25 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   const int lane = lane_id();
+  // the slot's state and its recorded path in one round trip (the path entries are valid
+  // memory whatever their contents; they are used only when a leaf is pending)
   const int leaf = p.g.leaf[g];
-  if (leaf < 0) return;
   const int half = p.g.half[g];
+  const int plen = p.g.path_len[g];
+  const int pn = p.g.path[(int64_t)g * kMaxPath + lane];
+  if (leaf < 0) return;
   const int64_t k = nidx(p, half, g, leaf);
   const uint64_t own = p.a.own[k], opp = p.a.opp[k], lg = p.a.legal[k];
   const bool is_root = leaf == 0;
+  // the path's N / W with the leaf's record (this kernel writes neither before the backup)
+  const bool on_path = plen > 0 && lane < plen;
+  int path_n = 0;
+  double path_w = 0.0;
+  if (on_path) {
+    const int64_t pk = nidx(p, half, g, pn);
+    path_n = p.a.N[pk];
+    path_w = p.a.W[pk];
+  }
 
   // ---- priors and value (MCTS_model.py:332-337)
   float pr, pr64;
@@ -555,12 +570,13 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
       p.a.flags[k] = p.a.flags[k] | kExpanded | (noise ? kChildF64 : 0);
     }
   }
-  // backup (MCTS_model.py:360) along the path k_select recorded
-  const int plen = p.g.path_len[g];
-  if (plen > 0) {
-    const int pn = lane < plen ? p.g.path[(int64_t)g * kMaxPath + lane] : 0;
-    backup_path(p, g, half, pn, plen - 1, v);
-  } else if (lane == 0) {
+  // backup (MCTS_model.py:360) along the path k_select recorded (backup_path's update on
+  // the values loaded above)
+  if (on_path) {
+    const int64_t pk = nidx(p, half, g, pn);
+    p.a.N[pk] = path_n + 1;
+    p.a.W[pk] = path_w + (((plen - 1 - lane) & 1) ? -v : v);
+  } else if (plen == 0 && lane == 0) {
     backup(p, g, half, leaf, v);
   }
   if (lane == 0) {
@@ -687,15 +703,27 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch) {
   }
   __syncthreads();
   // 2. pointer jumping until every link is 0 (member) or kOut; in-place updates only ever
-  // replace a link by one of its ancestors' links
+  // replace a link by one of its ancestors' links.  Each round jumps twice, and a thread
+  // keeps kU independent LDS reads in flight (the loop is LDS-latency-bound otherwise).
+  auto interior = [](uint16_t v) { return v != 0 && v != kOut; };
   for (;;) {
     int more = 0;
-    for (int j = tid; j < span; j += kMoveBlock) {
-      const uint16_t a = rel[j];
-      if (a != 0 && a != kOut) {
-        const uint16_t b = rel[a];
-        rel[j] = b;
-        more |= b != 0 && b != kOut;
+    for (int j0 = tid; j0 < span; j0 += kMoveBlock * kU) {
+      uint16_t a[kU], b[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int j = j0 + u * kMoveBlock;
+        a[u] = j < span ? rel[j] : (uint16_t)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) b[u] = interior(a[u]) ? rel[a[u]] : a[u];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) b[u] = interior(b[u]) ? rel[b[u]] : b[u];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int j = j0 + u * kMoveBlock;
+        if (j < span && b[u] != a[u]) rel[j] = b[u];
+        more |= interior(b[u]);
       }
     }
     if (!__syncthreads_or(more)) break;
@@ -1359,9 +1387,22 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
                           (int)e->lds_move) != hipSuccess) {
     (void)hipGetLastError();
   }
-  if (hipMemset(p.ctr, 0, sizeof(Counters)) != hipSuccess ||
-      hipMemset(p.g.status, 0, G * sizeof(int32_t)) != hipSuccess ||
-      hipMemset(p.g.leaf, 0xff, G * sizeof(int32_t)) != hipSuccess) {
+  // Every per-slot word and every node's flags / child count start zeroed (idle slots on
+  // half 0 with an unexpanded empty root): kernels that sweep all slots (k_root_stats,
+  // k_select's idle check, ...) read them before the host sets a slot up, and a reused
+  // device allocation would otherwise hold a previous engine's values (out-of-range
+  // halves, child ranges).
+  bool zero_ok = hipMemset(p.ctr, 0, sizeof(Counters)) == hipSuccess &&
+                 hipMemset(p.g.leaf, 0xff, G * sizeof(int32_t)) == hipSuccess &&
+                 hipMemset(p.a.flags, 0, nodes) == hipSuccess &&
+                 hipMemset(p.a.nchild, 0, nodes) == hipSuccess;
+  for (int32_t* a : {p.g.status, p.g.half, p.g.n_nodes, p.g.sims_done, p.g.sims_target,
+                     p.g.path_len, p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
+                     p.g.start_step, p.g.noise_cur, p.g.u_cur})
+    zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
+  zero_ok = zero_ok && hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
+            hipMemset(p.g.sym, 0, G) == hipSuccess;
+  if (!zero_ok) {
     free_all(e);
     delete e;
     return azc::set_error(AZ_ERR_HIP, "hipMemset failed");
