@@ -17,8 +17,11 @@ for C in [int(c) for c in os.environ.get("CS", "128").split(",")]:
     w9 = (torch.randn(9, C, C, device="cuda") / (3 * C ** 0.5)).contiguous()
     b = torch.zeros(C, device="cuda")
     y = torch.empty_like(x)
-    for exp in [int(v) for v in os.environ.get("EXPS", "0,1,2,4,8,16,32,7,23").split(",")]:
-        so = os.path.join(HERE, "_build", f"wino_exp{exp}.so")
+    for tag in os.environ.get("EXPS", "0,1,2,4,8,16,32,7,23").split(","):
+        # a tag is an AZ_WN_EXP value, optionally prefixed by a build name ("head0": the
+        # committed source, built beforehand into _build/wino_exphead0.so)
+        exp = int(tag.lstrip("abcdefghijklmnopqrstuvwxyz") or 0)
+        so = os.path.join(HERE, "_build", f"wino_exp{tag}.so")
         os.makedirs(os.path.dirname(so), exist_ok=True)
         if not os.path.exists(so):
             subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
@@ -41,7 +44,7 @@ for C in [int(c) for c in os.environ.get("CS", "128").split(",")]:
             for _ in range(30):
                 L.az_conv3x3_wino_gpu(*args)
             e1.record(); torch.cuda.synchronize()
-            key = f"C{C}_exp{exp}_mode{mode}"
+            key = f"C{C}_exp{tag}_mode{mode}"
             out[key] = round(e0.elapsed_time(e1) / 30 * 1e3, 1)
             if exp & 16:
                 stp = torch.as_strided(y, (4,), (1,)).clone().view(torch.int64)[:2].cpu().numpy()
