@@ -230,9 +230,10 @@ __device__ void emit_none(float* nn_in, int32_t* leaf_o, int g) {
 // one round trip per tree level suffices.
 struct NodeRec {
   int node;
-  int first;   // first child
-  int visits;  // N
-  int meta;    // flags | nchild << 8 | (uint8)tval << 16
+  int first;         // first child
+  int visits;        // N
+  int meta;          // flags | nchild << 8 | (uint8)tval << 16
+  uint64_t own, opp; // the position (the leaf's NN input, without another load)
 };
 
 __device__ __forceinline__ NodeRec load_rec(const Params& p, int g, int half, int node) {
@@ -242,6 +243,8 @@ __device__ __forceinline__ NodeRec load_rec(const Params& p, int g, int half, in
   r.first = p.a.first[k];
   r.visits = p.a.N[k];
   r.meta = (int)p.a.flags[k] | ((int)p.a.nchild[k] << 8) | ((int)(uint8_t)p.a.tval[k] << 16);
+  r.own = p.a.own[k];
+  r.opp = p.a.opp[k];
   return r;
 }
 __device__ __forceinline__ uint8_t rec_flags(const NodeRec& r) { return (uint8_t)r.meta; }
@@ -265,7 +268,7 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
   const double sq = sqrt((double)(par.visits + 1) + 1e-8);
   double score = -INFINITY;
   int idx = 0x7fffffff;
-  NodeRec mine{0, 0, 0, 0};
+  NodeRec mine{0, 0, 0, 0, 0ull, 0ull};
   if (lane < nc) {
     const int64_t c = nidx(p, half, g, fc + lane);
     const int n = p.a.N[c];
@@ -274,6 +277,8 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
     mine.first = p.a.first[c];
     mine.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
     mine.visits = n;
+    mine.own = p.a.own[c];
+    mine.opp = p.a.opp[c];
     const double q = -(n == 0 ? 0.0 : w / (double)n);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + n);
@@ -298,6 +303,8 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
   r.first = __shfl(mine.first, idx, kWave);
   r.visits = __shfl(mine.visits, idx, kWave);
   r.meta = __shfl(mine.meta, idx, kWave);
+  r.own = __shfl(mine.own, idx, kWave);
+  r.opp = __shfl(mine.opp, idx, kWave);
   return r;
 }
 
@@ -366,7 +373,6 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
     }
   }
   if (leaf >= 0) {
-    const int64_t k = nidx(p, half, g, leaf);
     int sym = 0;
     if (p.d4) {
       const uint32_t ev = p.g.rng_event[g];
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
         p.g.sym[g] = (uint8_t)sym;
       }
     }
-    emit_leaf(p, nn_in, g, p.a.own[k], p.a.opp[k], sym);
+    emit_leaf(p, nn_in, g, cur.own, cur.opp, sym);  // cur = the leaf's record
     if (depth < kMaxPath && lane <= depth) p.g.path[(int64_t)g * kMaxPath + lane] = path_node;
     if (lane == 0) {
       p.g.path_len[g] = depth < kMaxPath ? depth + 1 : 0;
@@ -652,6 +658,55 @@ __device__ float root_pi(const Params& p, int g, int half, double temp, double u
   return pi;
 }
 
+// root_pi on a root record already in registers: nc / legal of the root, `cnt` = this
+// lane's child visit count (lane j = child j) -- the same arithmetic as root_pi.
+__device__ float root_pi_pre(int nc, uint64_t lg, int cnt_lane, double temp, double u_tie,
+                             float* pi64) {
+  const int lane = lane_id();
+  float c = 0.0f, c64 = 0.0f;
+  if (nc > 0) {
+    const float cnt = lane < nc ? (float)cnt_lane : 0.0f;
+    const int src = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
+    const float cj = shfl(cnt, src);
+    if (lg) c = ((lg >> lane) & 1) ? cj : 0.0f;
+    else c64 = cj;
+  }
+  float pi, p64;
+  if (fabs(temp) < 1e-1) {
+    float m = fmaxf(c, c64);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, kWave));
+    const uint64_t ties = ballot(c == m);
+    const int k = azb::popc(ties) + (c64 == m ? 1 : 0);
+    int j = (int)(u_tie * (double)k);
+    j = j < 0 ? 0 : (j >= k ? k - 1 : j);
+    int best = 64;
+    if (j < azb::popc(ties)) {
+      uint64_t t = ties;
+      for (int i = 0; i < j; ++i) t &= t - 1;
+      best = __builtin_ctzll(t);
+    }
+    const bool any = nc > 0;  // `if len(self.root.valid_actions) != 0`
+    pi = (any && best == lane) ? 1.0f : 0.0f;
+    p64 = (any && best == 64) ? 1.0f : 0.0f;
+  } else {
+    const float ex = (float)(1.0 / temp);
+    const float ce = temp == 1.0 ? c : powf(c, ex);
+    const float ce64 = temp == 1.0 ? c64 : powf(c64, ex);
+    const float norm = np_sum65<float>(ce, ce64);
+    if (norm < (float)1e-12) {
+      const float u = nc > 0 ? (float)(1.0 / (double)nc) : 0.0f;
+      pi = (lg >> lane) & 1 ? u : 0.0f;
+      p64 = lg == 0 ? u : 0.0f;
+    } else {
+      pi = ce / norm;
+      p64 = ce64 / norm;
+    }
+  }
+  *pi64 = p64;
+  return pi;
+}
+
 // np.random.choice(65, p=pi) given its uniform draw u: cdf = cumsum(float64(pi)) (sequential),
 // cdf /= cdf[-1], searchsorted(u, side='right').  Lane 0 only; the second pass recomputes
 // the same sequential partial sums instead of keeping a 65-entry array in scratch.
@@ -896,55 +951,85 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
     const int ply = p.g.ply[g];
     const int player = p.g.root_player[g];
     if (tid < 64) {
-      // ---- pi (MCTS_model.py:244-271) and trajectory record (self_play_worker.py:72-73)
-      const double temp = ply < p.n_explore ? p.temp : 0.0;
-      double u_tie = 0.0;
-      if (fabs(temp) < 1e-1) {
-        double u = 0.0;
-        if (tid == 0) u = next_uniform(p, g, 0x1000u);
-        u_tie = shfl(u, 0);
+      // ---- one round trip for the root record and the slot's RNG cursor, one for the
+      // children's records (lane j = child j); everything after works from registers
+      const int64_t r = nidx(p, half, g, 0);
+      const int nc = p.a.nchild[r], fc = p.a.first[r];
+      const uint64_t lg = p.a.legal[r], r_own = p.a.own[r], r_opp = p.a.opp[r];
+      const int r_n = p.a.N[r];
+      const double r_w = p.a.W[r];
+      const bool injected = p.rng_mode == AZ_RNG_INJECTED;
+      const uint32_t rng0 = injected ? (uint32_t)p.g.u_cur[g] : p.g.rng_event[g];
+      int c_n = 0, c_flags = 0;
+      uint64_t c_own = 0, c_opp = 0;
+      if (tid < nc) {
+        const int64_t ck = nidx(p, half, g, fc + tid);
+        c_n = p.a.N[ck];
+        c_flags = p.a.flags[ck];
+        c_own = p.a.own[ck];
+        c_opp = p.a.opp[ck];
       }
+      // ---- the move's uniform draws (next_uniform, in draw order): the tie-break draw
+      // when temp < 0.1, then the action sample
+      const double temp = ply < p.n_explore ? p.temp : 0.0;
+      const bool tie_draw = fabs(temp) < 1e-1;
+      double u_tie = 0.0, u_act = 0.0;
+      if (tid == 0) {
+        auto draw = [&](uint32_t i, uint32_t sub) -> double {
+          if (injected) {
+            const uint32_t cur = rng0 + i;
+            return cur < (uint32_t)p.NU ? p.inj_u[(int64_t)g * p.NU + cur] : 0.5;
+          }
+          return azr::uniform1(p.seed, (uint32_t)g, rng0 + i, sub, p.stream_id);
+        };
+        if (tie_draw) u_tie = draw(0, 0x1000u);
+        u_act = draw(tie_draw ? 1 : 0, 0x2000u);
+        const uint32_t used = tie_draw ? 2u : 1u;
+        if (injected) p.g.u_cur[g] = (int)(rng0 + used);
+        else p.g.rng_event[g] = rng0 + used;
+      }
+      u_tie = shfl(u_tie, 0);
+      // ---- pi (MCTS_model.py:244-271) and trajectory record (self_play_worker.py:72-73)
       float p64;
-      const float pi = root_pi(p, g, half, temp, u_tie, &p64);
+      const float pi = root_pi_pre(nc, lg, c_n, temp, u_tie, &p64);
       s_pi[tid] = pi;
       if (tid == 0) s_pi[64] = p64;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __builtin_amdgcn_wave_barrier();
-      const int64_t r = nidx(p, half, g, 0);
       const bool room = ply < p.T;
       if (room) p.g.t_pi[((int64_t)g * p.T + ply) * 65 + tid] = pi;
+      // ---- action sample (self_play_worker.py:75) and the chosen child (MCTS.make_move,
+      // MCTS_model.py:200-215): the children are every legal action in ascending order (or
+      // the single pass), so the child's index follows from the root's legal mask
+      int jc = -1;
       if (tid == 0) {
         if (room) {
           p.g.t_pi[((int64_t)g * p.T + ply) * 65 + 64] = p64;
-          p.g.t_own[(int64_t)g * p.T + ply] = p.a.own[r];
-          p.g.t_opp[(int64_t)g * p.T + ply] = p.a.opp[r];
+          p.g.t_own[(int64_t)g * p.T + ply] = r_own;
+          p.g.t_opp[(int64_t)g * p.T + ply] = r_opp;
           p.g.t_player[(int64_t)g * p.T + ply] = (int8_t)player;
-          const int n = p.a.N[r];
-          p.g.t_vroot[(int64_t)g * p.T + ply] = n == 0 ? 0.0 : p.a.W[r] / (double)n;
+          p.g.t_vroot[(int64_t)g * p.T + ply] = r_n == 0 ? 0.0 : r_w / (double)r_n;
         }
-        // ---- action sample (self_play_worker.py:75)
-        const double u = next_uniform(p, g, 0x2000u);
-        const int a = sample_action(s_pi, u);
-        // ---- the move: re-root to that child (MCTS.make_move, MCTS_model.py:200-215)
-        // the children are every legal action in ascending order (or the single pass):
-        // the chosen one's index follows from the root's legal mask, no per-child loads
-        const int nc = p.a.nchild[r], fc = p.a.first[r];
-        const uint64_t lg = p.a.legal[r];
-        int child = -1;
+        const int a = sample_action(s_pi, u_act);
         if (nc > 0) {
           if (lg) {
-            if (a < 64 && ((lg >> a) & 1)) child = fc + azb::popc(lg & ((1ull << a) - 1ull));
+            if (a < 64 && ((lg >> a) & 1)) jc = azb::popc(lg & ((1ull << a) - 1ull));
           } else if (a == azb::kPass) {
-            child = fc;
+            jc = 0;
           }
         }
-        s_child = child;
+      }
+      jc = shfl(jc, 0);
+      const int src = jc >= 0 ? jc : 0;
+      const int ch_flags = shfl(c_flags, src);
+      const uint64_t ch_own = shfl(c_own, src), ch_opp = shfl(c_opp, src);
+      if (tid == 0) {
+        s_child = jc >= 0 ? fc + jc : -1;
         int term = 1, winner = 0;
-        if (child >= 0) {
-          const int64_t ck = nidx(p, half, g, child);
+        if (jc >= 0) {
           // get_value_and_terminated from the mover's view (self_play_worker.py:77-86)
-          term = (p.a.flags[ck] & kTerminal) ? 1 : 0;
-          const int d = azb::popc(p.a.opp[ck]) - azb::popc(p.a.own[ck]);
+          term = (ch_flags & kTerminal) ? 1 : 0;
+          const int d = azb::popc(ch_opp) - azb::popc(ch_own);
           winner = d > 0 ? player : (d < 0 ? -player : 0);
         }
         if (!room) term = 1;  // trajectory capacity exhausted (never at T >= 128)
