@@ -117,6 +117,21 @@ def make_net(kind):
     return AlphaZeroNet(8, 65, 5, 128) if kind == "az5x128" else FastOthelloNet(8, 65)
 
 
+def launch_ms(launch, reps):
+    """Average duration of one launch: a HIP event pair around each launch on its stream
+    (the current torch stream, which the entry points are given), so the figure is the
+    kernel's own duration -- the quantity rocprofv3 --kernel-trace reports -- and not the
+    back-to-back loop's inter-launch gaps."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for e0, e1 in evs:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize()
+    return sum(e0.elapsed_time(e1) for e0, e1 in evs) / reps
+
+
 def kernel_roofline(positions, n, device):
     """Time oth_step_gpu over n positions resident in HBM."""
     import az_native as nat
@@ -146,13 +161,7 @@ def kernel_roofline(positions, n, device):
         nat.check(nat.lib.oth_step_gpu(*args), "oth_step_gpu")
     torch.cuda.synchronize()
     reps_t = 20
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(reps_t):
-        nat.lib.oth_step_gpu(*args)
-    ev1.record()
-    torch.cuda.synchronize()
-    ms = ev0.elapsed_time(ev1) / reps_t
+    ms = launch_ms(lambda: nat.lib.oth_step_gpu(*args), reps_t)
     # spot-check the timed outputs against the host build of the same entry point
     k = min(n, 1 << 16)
     co, cp, cl, cs = nat.step_cpu(np.tile(own, reps)[:k], np.tile(opp, reps)[:k],
@@ -172,8 +181,11 @@ def conv_roofline(sp, device, n_boards):
 
     conv = sp.net.c2[0]
     C = conv.channels
-    x = torch.randn(n_boards, C, 8, 8, device=device).contiguous(memory_format=torch.channels_last)
-    r = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    # post-ReLU-like synthetic activations (about half zeros, as the trunk's inputs are):
+    # MFMA power -- and with it the clock the chip holds -- depends on the operand values
+    x = torch.randn(n_boards, C, 8, 8, device=device).relu().contiguous(
+        memory_format=torch.channels_last)
+    r = torch.randn_like(x).relu().contiguous(memory_format=torch.channels_last)
     y = torch.empty_like(x)
     if conv.precision == "fp32":
         fn = nat.lib.az_conv3x3_gpu
@@ -195,14 +207,7 @@ def conv_roofline(sp, device, n_boards):
     for _ in range(3):
         nat.check(fn(*args), kname)
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
-    ev0.record()
-    for _ in range(reps):
-        fn(*args)
-    ev1.record()
-    torch.cuda.synchronize()
-    ms = ev0.elapsed_time(ev1) / reps
+    ms = launch_ms(lambda: fn(*args), 50)
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
     out = {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
