@@ -7,11 +7,11 @@
 //   v = relu(conv1x1_{C->1}(h) + b)            v[pos]
 //   value = tanh(val_fc2(relu(val_fc1(v))))   (64 -> 256 -> 1)
 // One wavefront per board, four boards per workgroup: lane = board square for the 1x1
-// convs, lane = output for the FCs, whose weights (pre-transposed: pol_fc as [128][65],
-// val_fc1 as [64][256]) the workgroup stages in LDS once; every global load is issued
-// before the first use (the kernel is latency-bound, not bandwidth-bound); the per-board
-// vectors pass through LDS.  Replaces a MIOpen 1x1 conv, its
-// epilogue, two hipBLASLt GEMMs, softmax, ReLU/tanh kernels and two device copies per step.
+// convs, lane = output for the FCs, whose weights are pre-transposed (pol_fc as [128][65],
+// val_fc1 as [64][256]) and read from L2, where every workgroup finds them (STAGE = true
+// stages them in LDS per workgroup instead: measured slower); the per-board vectors pass
+// through LDS.  Replaces a MIOpen 1x1 conv, its epilogue, two hipBLASLt GEMMs, softmax,
+// ReLU/tanh kernels and two device copies per step.
 #include "common.h"
 
 namespace {
@@ -29,7 +29,7 @@ __device__ __forceinline__ float wave_max(float x) {
   return x;
 }
 
-template <int C>
+template <int C, bool STAGE = true>
 __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
     const float* __restrict__ h, const float* __restrict__ wpv, const float* __restrict__ bpv,
     const float* __restrict__ wpolT, const float* __restrict__ bpol,
@@ -38,8 +38,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
     int n_boards) {
   constexpr int kThreads = 64 * kWaves;
   constexpr int kPol = 128 * 65, kVal = 64 * 256;   // FC weight floats
-  __shared__ __align__(16) float s_wpol[kPol];      // pol_fc^T  [128][65]
-  __shared__ __align__(16) float s_w1[kVal];        // val_fc1^T [64][256]
+  __shared__ __align__(16) float s_wpol[STAGE ? kPol : 4];  // pol_fc^T  [128][65]
+  __shared__ __align__(16) float s_w1[STAGE ? kVal : 4];    // val_fc1^T [64][256]
+  const float* wpol = STAGE ? s_wpol : wpolT;  // !STAGE: straight from L2 (shared by all)
+  const float* w1s = STAGE ? s_w1 : w1T;
   __shared__ float s_p[kWaves][128];
   __shared__ float s_v[kWaves][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -49,26 +51,31 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
   // Every global load of the kernel is issued up front (one round trip, not one per loop
   // batch): the workgroup's FC weights (shared by its boards, staged to LDS) and this
   // lane's activation row (square `lane`: C floats).
-  constexpr int NP = (kPol / 4 + kThreads - 1) / kThreads, NV = kVal / 4 / kThreads;
+  constexpr int NP = STAGE ? (kPol / 4 + kThreads - 1) / kThreads : 1;
+  constexpr int NV = STAGE ? kVal / 4 / kThreads : 1;
   float4 wp[NP], wv[NV];
+  if (STAGE) {
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int q = i * kThreads + tid;
-    wp[i] = q < kPol / 4 ? reinterpret_cast<const float4*>(wpolT)[q] : make_float4(0, 0, 0, 0);
+    for (int i = 0; i < NP; ++i) {
+      const int q = i * kThreads + tid;
+      wp[i] = q < kPol / 4 ? reinterpret_cast<const float4*>(wpolT)[q] : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) wv[i] = reinterpret_cast<const float4*>(w1T)[i * kThreads + tid];
   }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) wv[i] = reinterpret_cast<const float4*>(w1T)[i * kThreads + tid];
   float4 x[C / 4];
   const float4* hp = reinterpret_cast<const float4*>(h + ((size_t)(live ? b : 0) * 64 + lane) * C);
 #pragma unroll
   for (int c = 0; c < C / 4; ++c) x[c] = hp[c];
+  if (STAGE) {
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int q = i * kThreads + tid;
-    if (q < kPol / 4) reinterpret_cast<float4*>(s_wpol)[q] = wp[i];
+    for (int i = 0; i < NP; ++i) {
+      const int q = i * kThreads + tid;
+      if (q < kPol / 4) reinterpret_cast<float4*>(s_wpol)[q] = wp[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) reinterpret_cast<float4*>(s_w1)[i * kThreads + tid] = wv[i];
   }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) reinterpret_cast<float4*>(s_w1)[i * kThreads + tid] = wv[i];
 
   // 1x1 convs (policy 2 channels, value 1 channel) at square `lane`
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
@@ -91,9 +98,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
   // policy FC: lane a -> logit a; logit 64 split over the lanes and reduced
   float la = bpol[lane];
 #pragma unroll 16
-  for (int k = 0; k < 128; ++k) la += s_wpol[k * 65 + lane] * s_p[w][k];
-  float l64 = s_wpol[lane * 65 + 64] * s_p[w][lane] +
-              s_wpol[(lane + 64) * 65 + 64] * s_p[w][lane + 64];
+  for (int k = 0; k < 128; ++k) la += wpol[k * 65 + lane] * s_p[w][k];
+  float l64 = wpol[lane * 65 + 64] * s_p[w][lane] + wpol[(lane + 64) * 65 + 64] * s_p[w][lane + 64];
   l64 = wave_sum(l64) + bpol[64];
   const float m = fmaxf(wave_max(la), l64);
   const float e = __expf(la - m), e64 = __expf(l64 - m);
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
   float4 acc = reinterpret_cast<const float4*>(b1)[lane];
 #pragma unroll 16
   for (int i = 0; i < 64; ++i) {
-    const float4 wq = reinterpret_cast<const float4*>(s_w1 + i * 256)[lane];
+    const float4 wq = reinterpret_cast<const float4*>(w1s + i * 256)[lane];
     const float vi = s_v[w][i];
     acc.x += wq.x * vi;
     acc.y += wq.y * vi;
@@ -135,12 +141,14 @@ extern "C" int az_heads_az_gpu(const float* h, const float* wpv, const float* bp
              AZ_ERR_ARG, "az_heads_az_gpu: buffers must be 16-byte aligned");
   hipStream_t s = azc::as_stream(stream);
   const unsigned grid = (unsigned)((n_boards + kWaves - 1) / kWaves);
+  // FC weights read straight from L2 (shared by every workgroup): measured 15.3-15.6 us
+  // against 16.8-17.8 us staging them in LDS per workgroup (scripts/exp/heads_ab.py)
   if (channels == 128)
-    hipLaunchKernelGGL(k_heads_az<128>, dim3(grid), dim3(64 * kWaves), 0, s, h, wpv, bpv, wpolT,
-                       bpol, w1T, b1, w2, b2, priors, values, n_boards);
+    hipLaunchKernelGGL((k_heads_az<128, false>), dim3(grid), dim3(64 * kWaves), 0, s, h, wpv,
+                       bpv, wpolT, bpol, w1T, b1, w2, b2, priors, values, n_boards);
   else if (channels == 64)
-    hipLaunchKernelGGL(k_heads_az<64>, dim3(grid), dim3(64 * kWaves), 0, s, h, wpv, bpv, wpolT,
-                       bpol, w1T, b1, w2, b2, priors, values, n_boards);
+    hipLaunchKernelGGL((k_heads_az<64, false>), dim3(grid), dim3(64 * kWaves), 0, s, h, wpv,
+                       bpv, wpolT, bpol, w1T, b1, w2, b2, priors, values, n_boards);
   else
     return azc::set_error(AZ_ERR_ARG, "az_heads_az_gpu: channels must be 64 or 128, got %d",
                           channels);
