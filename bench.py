@@ -28,10 +28,11 @@ the window are reported beside it.
 
 Also measured in the same run:
   roofline      the bitboard-step kernel (oth_step_gpu, the north-star kernel) on 2^24
-                positions drawn from this run's self-play states: 43 algorithmic bytes per
+                positions of seeded random playouts, timed before the
+                self-play warmup and again after the window: 43 algorithmic bytes per
                 position (read own, opp, act = 17; write own', opp', legal, status = 26),
                 HIP events on the launch stream; traffic = HBM bytes from rocprofv3 PMC
-                (profiles/), or null.
+                (profiles/oth_step_traffic.json), or null.
   cpu_baseline  the oracle's restatement of the reference self-play (oracle/selfplay.py:
                 sequential MCTS, batch-1 torch-CPU inference of the same net, the C board
                 oracle) on 1 host core for a bounded sample of moves.
@@ -132,42 +133,68 @@ def launch_ms(launch, reps):
     return sum(e0.elapsed_time(e1) for e0, e1 in evs) / reps
 
 
-def kernel_roofline(positions, n, device):
-    """Time oth_step_gpu over n positions resident in HBM."""
+def playout_positions(games=4096, plies=60, seed=0xC0FFEE):
+    """SURVEY.md 8(d)'s kernel-bench inputs: positions of seeded uniform-random playouts from
+    the initial position (one per game and ply, plies 0..59, finished games dropped), each
+    with one uniformly drawn legal action (or the pass).  Played on the product's host entry
+    points (oth_legal_cpu / oth_step_cpu, the same bitboard.h code as the kernel)."""
     import az_native as nat
 
-    own, opp = positions
-    rng = np.random.default_rng(0)
-    # one legal action (or pass) per distinct position, then tile to n
-    lg = nat.legal_cpu(own, opp)
-    act = np.empty(len(own), np.uint8)
-    for i, m in enumerate(lg):
-        m = int(m)
-        if m == 0:
-            act[i] = 64
-        else:
-            bits = [b for b in range(64) if (m >> b) & 1]
-            act[i] = bits[int(rng.integers(0, len(bits)))]
-    reps = -(-n // len(own))
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.tile(a, reps)[:n])).to(device)
-    d_own, d_opp = t(own.view(np.int64)), t(opp.view(np.int64))
-    d_act = t(act)
-    outs = [torch.empty(n, dtype=torch.int64, device=device) for _ in range(3)]
-    st = torch.empty(n, dtype=torch.int16, device=device)
-    s = nat.stream_ptr()
-    args = [nat.ptr(d_own), nat.ptr(d_opp), nat.ptr(d_act)] + [nat.ptr(x) for x in outs] + \
-        [nat.ptr(st), n, s]
-    for _ in range(3):
-        nat.check(nat.lib.oth_step_gpu(*args), "oth_step_gpu")
-    torch.cuda.synchronize()
-    reps_t = 20
-    ms = launch_ms(lambda: nat.lib.oth_step_gpu(*args), reps_t)
-    # spot-check the timed outputs against the host build of the same entry point
-    k = min(n, 1 << 16)
-    co, cp, cl, cs = nat.step_cpu(np.tile(own, reps)[:k], np.tile(opp, reps)[:k],
-                                  np.tile(act, reps)[:k], raise_illegal=False)
-    assert (outs[0][:k].cpu().numpy().view(np.uint64) == co).all()
-    return ms, n
+    rng = np.random.default_rng(seed)
+    own = np.full(games, 0x0000000810000000, np.uint64)
+    opp = np.full(games, 0x0000001008000000, np.uint64)
+    live = np.ones(games, bool)
+    P, O, A = [], [], []
+    bitv = (np.uint64(1) << np.arange(64, dtype=np.uint64))
+    for _ in range(plies):
+        lg = nat.legal_cpu(own, opp)
+        bits = (lg[:, None] & bitv[None, :]) != 0
+        # uniform legal placement: argmax of random keys over the set bits; none -> pass
+        keys = np.where(bits, rng.random(bits.shape), -1.0)
+        act = np.where(bits.any(1), keys.argmax(1), 64).astype(np.uint8)
+        P.append(own[live]), O.append(opp[live]), A.append(act[live])
+        no, np_, _, st = nat.step_cpu(own, opp, act)
+        own, opp = no, np_
+        live &= (st & 1) == 0  # terminal flag: the game is over
+        if not live.any():
+            break
+    return np.concatenate(P), np.concatenate(O), np.concatenate(A)
+
+
+class StepKernelBench:
+    """oth_step_gpu over n positions resident in HBM (the playout corpus tiled to n)."""
+
+    def __init__(self, n, device):
+        import az_native as nat
+
+        self.nat, self.n = nat, n
+        own, opp, act = playout_positions()
+        self.host = (own, opp, act)
+        reps = -(-n // len(own))
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(np.tile(a, reps)[:n])).to(device)
+        self.inp = (t(own.view(np.int64)), t(opp.view(np.int64)), t(act))
+        self.outs = [torch.empty(n, dtype=torch.int64, device=device) for _ in range(3)]
+        self.st = torch.empty(n, dtype=torch.int16, device=device)
+        self.args = [nat.ptr(x) for x in self.inp] + [nat.ptr(x) for x in self.outs] + \
+            [nat.ptr(self.st), n, nat.stream_ptr()]
+
+    def time_ms(self, reps=20):
+        nat = self.nat
+        for _ in range(3):
+            nat.check(nat.lib.oth_step_gpu(*self.args), "oth_step_gpu")
+        torch.cuda.synchronize()
+        ms = launch_ms(lambda: nat.lib.oth_step_gpu(*self.args), reps)
+        # spot-check the timed outputs against the host build of the same entry point
+        own, opp, act = self.host
+        k = min(self.n, len(own))
+        co, cp, cl, cs = nat.step_cpu(own[:k], opp[:k], act[:k], raise_illegal=False)
+        assert (self.outs[0][:k].cpu().numpy().view(np.uint64) == co).all()
+        assert (self.outs[2][:k].cpu().numpy().view(np.uint64) == cl).all()
+        assert (self.st[:k].cpu().numpy().view(np.uint16) == cs).all()
+        return ms
+
+    def release(self):
+        self.inp = self.outs = self.st = self.args = None
 
 
 def conv_roofline(sp, device, n_boards):
@@ -317,6 +344,13 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    # the north-star kernel first, with the chip in the state the profiler run also sees it
+    # in (rocprofv3 serialises the self-play, which then heats the chip less): the figure
+    # agrees with the committed rocprof summary; it is re-timed after the window below
+    kb = None
+    if rank == 0 and world == 1 and not a.skip_kernel:
+        kb = StepKernelBench(a.kernel_n, device)
+        ms_step_kernel = kb.time_ms()
     sp.step(warmup_run)
     barrier()
     c0 = e.counters()
@@ -385,12 +419,10 @@ def main():
                    "window_s": round(t_max, 3), "allgather_rows": allgather_rows,
                    "arena_overflows": int(c1["arena_overflows"])},
     }
-    if rank == 0 and world == 1 and not a.skip_kernel:
-        smp = e.samples(0, min(c1["samples"], 200000))
-        if len(smp["own"]) < 1024:
-            smp = {"own": np.array([0x0000000810000000], np.uint64),
-                   "opp": np.array([0x0000001008000000], np.uint64)}
-        ms, n = kernel_roofline((smp["own"], smp["opp"]), a.kernel_n, device)
+    if kb is not None:
+        ms, n = ms_step_kernel, a.kernel_n
+        ms_hot = kb.time_ms()
+        kb.release()
         achieved = STEP_BYTES * n / (ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(a.traffic_json):
@@ -404,7 +436,12 @@ def main():
                               "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
                               "traffic": traffic, "positions": n,
                               "avg_launch_ms": round(ms, 4),
-                              "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
+                              "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2),
+                              "inputs": "seeded random playouts (SURVEY.md 8d: seed 0xC0FFEE, "
+                                        "plies 0-59, one legal action each), tiled to 2^24",
+                              "avg_launch_ms_after_selfplay": round(ms_hot, 4),
+                              "frac_after_selfplay": round(STEP_BYTES * n / (ms_hot * 1e-3)
+                                                           / 1e9 / HBM_PEAK_GBS, 4)}
     if rank == 0 and world == 1 and not a.skip_kernel and hasattr(sp.net, "c2") \
             and getattr(sp.net, "conv_impl", "") == "hip":
         result["roofline_conv"] = conv_roofline(sp, device, a.games)

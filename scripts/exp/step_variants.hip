@@ -535,11 +535,74 @@ __global__ __launch_bounds__(256) void v34(const uint64_t* own, const uint64_t* 
   step33<false>(rays, own, opp, act, oo, po, lo, so, (uint32_t)n);
 }
 
+// v35: v33 with the per-ray validity as a sign mask: xo = x & own is 0 or one bit, so the
+// top bit of -xo is (xo != 0); its arithmetic-shifted high word masks R & d in one bitop3
+// per half (no compare / select pair per ray)
+__device__ __forceinline__ uint64_t ray_flips_s(uint64_t R, uint64_t own, uint64_t nopp) {
+  using namespace azb::tt;
+  const uint64_t o = R & nopp;
+  const uint64_t d = o - 1ull;
+  const uint64_t xo = azb::bop3<A & ~B & C>(o, d, own);
+  const uint32_t m = xo != 0ull ? 0xFFFFFFFFu : 0u;
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)R, (uint32_t)d, m, A & B & C);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(R >> 32), (uint32_t)(d >> 32), m, A & B & C);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ azb::Move move35(const uint64_t* rays, uint64_t own, uint64_t opp, int act) {
+  const int sq = act & 63;
+  const uint64_t nb = 1ull << sq;
+  const uint64_t* up = rays + 4 * sq;
+  const uint64_t* upr = rays + 4 * (63 - sq);
+  const uint64_t nopp = ~opp, ownr = azb::rev64(own), noppr = azb::rev64(nopp);
+  const uint64_t fu = ray_flips_s(up[0], own, nopp) | ray_flips_s(up[1], own, nopp) |
+                      ray_flips_s(up[2], own, nopp) | ray_flips_s(up[3], own, nopp);
+  const uint64_t fd = ray_flips_s(upr[0], ownr, noppr) | ray_flips_s(upr[1], ownr, noppr) |
+                      ray_flips_s(upr[2], ownr, noppr) | ray_flips_s(upr[3], ownr, noppr);
+  const uint64_t cap = fu | azb::rev64(fd);
+  const bool place = (unsigned)act < 64u && cap != 0ull && !(nb & (own | opp));
+  const bool pass = act == azb::kPass;
+  const uint64_t c = place ? cap : 0ull, b = place ? nb : 0ull;
+  azb::Move m;
+  m.illegal = !(place || pass);
+  m.flags = pass ? azb::kFlagPassed : 0;
+  m.own = m.illegal ? own : opp ^ c;
+  m.opp = m.illegal ? opp : azb::bop3<azb::tt::A ^ azb::tt::B ^ azb::tt::C>(own, b, c);
+  return m;
+}
+__global__ __launch_bounds__(256) void v35(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const uint32_t n = (uint32_t)n_;
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t n_pad = (n + 255) / 256 * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    const uint32_t o8 = i * 8u;
+    uint64_t o = 0, p = 0; int a = azb::kPass;
+    if (live) {
+      o = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(own) + o8);
+      p = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(opp) + o8);
+      a = act[i];
+    }
+    const azb::Move mv = move35(rays, o, p, a);
+    const bool ok = live && !mv.illegal;
+    const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+    int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+    tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+    if (live) {
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(oo) + o8) = mv.own;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(po) + o8) = mv.opp;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lo) + o8) = lg;
+      *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(so) + i * 2u) = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(mv.flags | tf, azb::popc(mv.own) - azb::popc(mv.opp));
+    }
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34};
-  if (v < 0 || v > 34) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35};
+  if (v < 0 || v > 35) return -1;
   const int blk = v == 14 ? 64 : 256;
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
