@@ -178,9 +178,13 @@ class StepKernelBench:
         self.args = [nat.ptr(x) for x in self.inp] + [nat.ptr(x) for x in self.outs] + \
             [nat.ptr(self.st), n, nat.stream_ptr()]
 
-    def time_ms(self, reps=20):
+    def time_ms(self, warm=400, reps=100):
+        """Average launch time at steady state: `warm` untimed back-to-back launches first
+        (the chip's power management takes ~8-200 launches of sustained load to settle
+        from a cold start, during which launches run up to 40 % slower:
+        profiles/r01_step_steady.json), then `reps` launches, each timed by its own event pair."""
         nat = self.nat
-        for _ in range(3):
+        for _ in range(warm):
             nat.check(nat.lib.oth_step_gpu(*self.args), "oth_step_gpu")
         torch.cuda.synchronize()
         ms = launch_ms(lambda: nat.lib.oth_step_gpu(*self.args), reps)
@@ -231,10 +235,10 @@ def conv_roofline(sp, device, n_boards):
         else:
             kname = f"k_conv3x3_mx (az_conv3x3_mx_gpu, {conv.precision})"
         peak = MFMA16_PEAK
-    for _ in range(3):
+    for _ in range(400):  # past the power-management transient (StepKernelBench.time_ms)
         nat.check(fn(*args), kname)
     torch.cuda.synchronize()
-    ms = launch_ms(lambda: fn(*args), 50)
+    ms = launch_ms(lambda: fn(*args), 100)
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
     out = {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",

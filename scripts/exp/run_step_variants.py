@@ -27,21 +27,28 @@ for v in VARS:
         args = [v] + [x.data_ptr() for x in I + O] + [n, grid, torch.cuda.current_stream().cuda_stream]
         assert L.run_variant(*args) == 0
         torch.cuda.synchronize()
+        # past the chip's power-management transient (launches ~8-200 of a cold start run
+        # slower; scripts/step_steady.py), then the steady state
+        for _ in range(int(os.environ.get('WARM', '400'))):
+            L.run_variant(*args)
         e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        NT = int(os.environ.get('TIMED', '200'))
         e0.record()
-        for _ in range(20):
+        for _ in range(NT):
             L.run_variant(*args)
         e1.record(); torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 20
+        ms = e0.elapsed_time(e1) / NT
         ok = None
-        if v in (0, 2, 3, 7, 9, 11, 13, 14, 16, 17, 18, 21, 22, 23, 24, 25, 26, 32, 33, 34, 35):
+        if v in (0, 2, 3, 7, 9, 11, 13, 14, 16, 17, 18, 21, 22, 23, 24, 25, 26, 32, 33, 34, 35, 36, 39, 40, 41):
             outs = [o.cpu() for o in O]
             if ref is None: ref = outs
             ok = all(bool((a == b).all()) for a, b in zip(outs, ref))
         if v in (5, 6):
             ok = bool((O[2].cpu() == ref[2]).all()) if False else None
-        res[f"v{v}_g{grid}"] = {"ms": round(ms, 4), "gsteps": round(n / ms / 1e6, 1), "alg_TBps": round(43 * n / ms / 1e9, 3), "ok": ok}
+        key = f"v{v}_g{grid}"
+        while key in res: key += "+"
+        res[key] = {"ms": round(ms, 4), "gsteps": round(n / ms / 1e6, 1), "alg_TBps": round(43 * n / ms / 1e9, 3), "ok": ok}
         if v in (29, 30, 31):
             st = O[2][n - 4:].cpu().numpy()
-            res[f"v{v}_g{grid}"]["clock_GHz"] = round(float(st[1] - st[0]) / float(st[3] - st[2]) * 0.1, 3)
+            res[key]["clock_GHz"] = round(float(st[1] - st[0]) / float(st[3] - st[2]) * 0.1, 3)
 print(json.dumps(res, indent=0))

@@ -598,11 +598,141 @@ __global__ __launch_bounds__(256) void v35(const uint64_t* own, const uint64_t* 
   }
 }
 
+// v36: the product body (branch-free move, cooperative terminal check), two consecutive
+// positions per lane: 16-byte own/opp/out accesses, 2-byte act, 4-byte status
+__device__ __forceinline__ void body36(const uint64_t* rays, uint64_t o, uint64_t p, int a, bool live,
+                                       uint64_t& no, uint64_t& np, uint64_t& lg, uint16_t& st) {
+  const azb::Move mv = azb::move_rays_bf(rays, o, p, a);
+  const bool ok = live && !mv.illegal;
+  lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+  int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+  tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+  no = mv.own; np = mv.opp;
+  st = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(mv.flags | tf, azb::popc(mv.own) - azb::popc(mv.opp));
+}
+__global__ __launch_bounds__(256) void v36(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t n_pad = (n2 + 255) / 256 * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n_pad; j += stride) {
+    const bool live = j < n2;
+    ulonglong2 a = make_ulonglong2(0, 0), b = make_ulonglong2(0, 0);
+    uint32_t c = 0x4040;
+    if (live) {
+      a = *reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(own) + j * 16u);
+      b = *reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(opp) + j * 16u);
+      c = *reinterpret_cast<const uint16_t*>(act + j * 2u);
+    }
+    uint64_t o0, p0, l0, o1, p1, l1; uint16_t s0, s1;
+    body36(rays, a.x, b.x, c & 0xFF, live, o0, p0, l0, s0);
+    body36(rays, a.y, b.y, c >> 8, live, o1, p1, l1, s1);
+    if (live) {
+      *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(oo) + j * 16u) = make_ulonglong2(o0, o1);
+      *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(po) + j * 16u) = make_ulonglong2(p0, p1);
+      *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(lo) + j * 16u) = make_ulonglong2(l0, l1);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(so) + j * 4u) = (uint32_t)s0 | ((uint32_t)s1 << 16);
+    }
+  }
+}
+// v37: I/O only in v36's pattern
+__global__ __launch_bounds__(256) void v37(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n2; j += stride) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(own) + j * 16u);
+    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(opp) + j * 16u);
+    const uint32_t c = *reinterpret_cast<const uint16_t*>(act + j * 2u);
+    *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(oo) + j * 16u) = make_ulonglong2(a.x ^ c, a.y);
+    *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(po) + j * 16u) = b;
+    *reinterpret_cast<ulonglong2*>(reinterpret_cast<char*>(lo) + j * 16u) = make_ulonglong2(a.x | b.x, a.y | b.y);
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(so) + j * 4u) = c * 3u;
+  }
+}
+// v38: I/O only, one position per lane, plain stores, 32-bit offsets (the product's pattern)
+__global__ __launch_bounds__(256) void v38(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  const uint32_t n = (uint32_t)n_;
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t a = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(own) + i * 8u);
+    const uint64_t b = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(opp) + i * 8u);
+    const uint32_t c = act[i];
+    *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(oo) + i * 8u) = a ^ c;
+    *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(po) + i * 8u) = b;
+    *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lo) + i * 8u) = a | b;
+    *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(so) + i * 2u) = (uint16_t)(c * 3u);
+  }
+}
+
+// v39 / v41: v36 with non-temporal stores (v41: and non-temporal loads); v40: v33 with
+// non-temporal stores
+typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+template <bool NTL>
+__device__ __forceinline__ void step39(const uint64_t* rays, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t n_pad = (n2 + 255) / 256 * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n_pad; j += stride) {
+    const bool live = j < n2;
+    u64x2v a = {0, 0}, b = {0, 0};
+    uint32_t c = 0x4040;
+    if (live) {
+      const u64x2v* pa = reinterpret_cast<const u64x2v*>(reinterpret_cast<const char*>(own) + j * 16u);
+      const u64x2v* pb = reinterpret_cast<const u64x2v*>(reinterpret_cast<const char*>(opp) + j * 16u);
+      if (NTL) { a = __builtin_nontemporal_load(pa); b = __builtin_nontemporal_load(pb); }
+      else { a = *pa; b = *pb; }
+      c = *reinterpret_cast<const uint16_t*>(act + j * 2u);
+    }
+    uint64_t o0, p0, l0, o1, p1, l1; uint16_t s0, s1;
+    body36(rays, a.x, b.x, c & 0xFF, live, o0, p0, l0, s0);
+    body36(rays, a.y, b.y, c >> 8, live, o1, p1, l1, s1);
+    if (live) {
+      u64x2v vo = {o0, o1}, vp = {p0, p1}, vl = {l0, l1};
+      __builtin_nontemporal_store(vo, reinterpret_cast<u64x2v*>(reinterpret_cast<char*>(oo) + j * 16u));
+      __builtin_nontemporal_store(vp, reinterpret_cast<u64x2v*>(reinterpret_cast<char*>(po) + j * 16u));
+      __builtin_nontemporal_store(vl, reinterpret_cast<u64x2v*>(reinterpret_cast<char*>(lo) + j * 16u));
+      __builtin_nontemporal_store((uint32_t)s0 | ((uint32_t)s1 << 16), reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(so) + j * 4u));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void v39(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  step39<false>(rays, own, opp, act, oo, po, lo, so, n);
+}
+__global__ __launch_bounds__(256) void v41(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  step39<true>(rays, own, opp, act, oo, po, lo, so, n);
+}
+__global__ __launch_bounds__(256) void v40(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const uint32_t n = (uint32_t)n_;
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t n_pad = (n + 255) / 256 * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_pad; i += stride) {
+    const bool live = i < n;
+    uint64_t o = 0, p = 0; int a = azb::kPass;
+    if (live) { o = own[i]; p = opp[i]; a = act[i]; }
+    uint64_t no, np, lg; uint16_t st;
+    body36(rays, o, p, a, live, no, np, lg, st);
+    if (live) {
+      __builtin_nontemporal_store(no, oo + i); __builtin_nontemporal_store(np, po + i);
+      __builtin_nontemporal_store(lg, lo + i); __builtin_nontemporal_store(st, so + i);
+    }
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35};
-  if (v < 0 || v > 35) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41};
+  if (v < 0 || v > 41) return -1;
   const int blk = v == 14 ? 64 : 256;
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
