@@ -34,12 +34,89 @@ namespace {
 constexpr int kBlock = 256;
 static_assert(kBlock == 64 * 4, "k_step stages one up-ray per thread");
 
-// One position per lane per iteration, grid-stride.  Every global access is a
-// lane-contiguous 8-byte (own/opp/legal), 1-byte (act) or 2-byte (status) access, so a
-// wave moves 64 consecutive positions per instruction; 32-bit byte offsets off the
-// uniform array bases (n < 2^28: the host checks) keep address math off the 64-bit VALU.
-// The capture set comes from the 2 KB up-ray table staged once per workgroup in LDS (two
-// ds_read_b128 per ray set); the make-move is branch-free (move_rays_bf).
+// The board step of one position (the body of both k_step forms): branch-free make-move
+// with the capture set from the LDS up-ray table, the next side's legal mask, the
+// wave-cooperative terminal check (every lane of the wave must call it: uniform control
+// flow) and the status word.
+__device__ __forceinline__ void step_one(const uint64_t* rays, uint64_t o, uint64_t p, int a,
+                                         bool live, uint64_t& no, uint64_t& np, uint64_t& lg,
+                                         uint16_t& st) {
+  const azb::Move mv = azb::move_rays_bf(rays, o, p, a);
+  const bool ok = live && !mv.illegal;
+  lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
+  int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
+  tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+  no = mv.own;
+  np = mv.opp;
+  st = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0)
+                  : azb::pack_status(mv.flags | tf, azb::popc(mv.own) - azb::popc(mv.opp));
+}
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// Two consecutive positions per lane per iteration, grid-stride: every global access is a
+// lane-contiguous 16-byte (own/opp/legal pairs), 2-byte (act pair) or 4-byte (status pair)
+// access, non-temporal (each byte is touched once), 32-bit byte offsets off the uniform
+// array bases (n < 2^28: the host checks).  Measured at steady state on 2^24 positions
+// (scripts/exp/step_variants.hip v41 vs v33): 0.137 vs 0.145 ms for the one-position,
+// 8-byte, write-back form below.  Needs 16-byte aligned own/opp/out arrays, a 2-byte
+// aligned act and a 4-byte aligned status array (the host checks); an odd n leaves the
+// last position to the lane whose pair is half live.
+__global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ own,
+                                                  const uint64_t* __restrict__ opp,
+                                                  const uint8_t* __restrict__ act,
+                                                  uint64_t* __restrict__ own_o,
+                                                  uint64_t* __restrict__ opp_o,
+                                                  uint64_t* __restrict__ legal_o,
+                                                  uint16_t* __restrict__ status_o,
+                                                  uint32_t n) {
+  __shared__ __align__(16) uint64_t rays[64 * 4];
+  rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
+  __syncthreads();
+  const uint32_t pairs = (n + 1) / 2, full = n / 2;
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t p_pad = (pairs + kBlock - 1) / kBlock * kBlock;
+  const char* own_b = reinterpret_cast<const char*>(own);
+  const char* opp_b = reinterpret_cast<const char*>(opp);
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < p_pad; j += stride) {
+    const uint32_t o16 = j * 16u;
+    u64x2 a = {0ull, 0ull}, b = {0ull, 0ull};
+    uint32_t c = azb::kPass | (azb::kPass << 8);
+    const bool live0 = j < pairs, live1 = j < full;
+    if (live1) {
+      a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(own_b + o16));
+      b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(opp_b + o16));
+      c = *reinterpret_cast<const uint16_t*>(act + 2u * j);
+    } else if (live0) {  // odd n: the last position alone
+      a.x = *reinterpret_cast<const uint64_t*>(own_b + o16);
+      b.x = *reinterpret_cast<const uint64_t*>(opp_b + o16);
+      c = act[2u * j] | (azb::kPass << 8);
+    }
+    uint64_t o0, p0, l0, o1, p1, l1;
+    uint16_t s0, s1;
+    step_one(rays, a.x, b.x, c & 0xFF, live0, o0, p0, l0, s0);
+    step_one(rays, a.y, b.y, c >> 8, live1, o1, p1, l1, s1);
+    char* oo = reinterpret_cast<char*>(own_o) + o16;
+    char* po = reinterpret_cast<char*>(opp_o) + o16;
+    char* lo = reinterpret_cast<char*>(legal_o) + o16;
+    if (live1) {
+      const u64x2 vo = {o0, o1}, vp = {p0, p1}, vl = {l0, l1};
+      __builtin_nontemporal_store(vo, reinterpret_cast<u64x2*>(oo));
+      __builtin_nontemporal_store(vp, reinterpret_cast<u64x2*>(po));
+      __builtin_nontemporal_store(vl, reinterpret_cast<u64x2*>(lo));
+      __builtin_nontemporal_store((uint32_t)s0 | ((uint32_t)s1 << 16),
+                                  reinterpret_cast<uint32_t*>(status_o) + j);
+    } else if (live0) {
+      *reinterpret_cast<uint64_t*>(oo) = o0;
+      *reinterpret_cast<uint64_t*>(po) = p0;
+      *reinterpret_cast<uint64_t*>(lo) = l0;
+      status_o[2u * j] = s0;
+    }
+  }
+}
+
+// One position per lane per iteration (any alignment): lane-contiguous 8-byte
+// (own/opp/legal), 1-byte (act) and 2-byte (status) accesses.
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ own,
                                                  const uint64_t* __restrict__ opp,
                                                  const uint8_t* __restrict__ act,
@@ -66,18 +143,14 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
       p = *reinterpret_cast<const uint64_t*>(opp_b + o8);
       a = act[i];
     }
-    const azb::Move mv = azb::move_rays_bf(rays, o, p, a);
-    const bool ok = live && !mv.illegal;
-    const uint64_t lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
-    int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
-    tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+    uint64_t no, np, lg;
+    uint16_t st;
+    step_one(rays, o, p, a, live, no, np, lg, st);
     if (live) {
-      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(own_o) + o8) = mv.own;
-      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(opp_o) + o8) = mv.opp;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(own_o) + o8) = no;
+      *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(opp_o) + o8) = np;
       *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(legal_o) + o8) = lg;
-      status_o[i] = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0)
-                               : azb::pack_status(mv.flags | tf,
-                                                  azb::popc(mv.own) - azb::popc(mv.opp));
+      status_o[i] = st;
     }
   }
 }
@@ -234,8 +307,17 @@ int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
              "oth_step_gpu: null buffer");
   AZ_REQUIRE(n < (int64_t(1) << 28), AZ_ERR_ARG,
              "oth_step_gpu: n=%lld exceeds 2^28 positions per call", (long long)n);
-  hipLaunchKernelGGL(k_step, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
-                     own, opp, act, own_o, opp_o, legal_o, status_o, (uint32_t)n);
+  const auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
+  const bool paired = a16(own) && a16(opp) && a16(own_o) && a16(opp_o) && a16(legal_o) &&
+                      (reinterpret_cast<uintptr_t>(act) & 1u) == 0 &&
+                      (reinterpret_cast<uintptr_t>(status_o) & 3u) == 0;
+  if (paired)
+    hipLaunchKernelGGL(k_step2, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0,
+                       azc::as_stream(stream), own, opp, act, own_o, opp_o, legal_o, status_o,
+                       (uint32_t)n);
+  else
+    hipLaunchKernelGGL(k_step, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
+                       own, opp, act, own_o, opp_o, legal_o, status_o, (uint32_t)n);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

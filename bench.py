@@ -434,7 +434,7 @@ def main():
                 traffic = json.load(open(a.traffic_json)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        result["roofline"] = {"kernel": "oth_step_gpu (k_step)", "bound": "hbm",
+        result["roofline"] = {"kernel": "oth_step_gpu (k_step2, two positions per lane)", "bound": "hbm",
                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                               "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),

@@ -728,12 +728,59 @@ __global__ __launch_bounds__(256) void v40(const uint64_t* own, const uint64_t* 
   }
 }
 
+// v42: v41 with two pairs per lane per iteration (pairs j and j + stride/2... as two
+// grid-stride streams): both pairs' loads issued before either is computed
+__global__ __launch_bounds__(256) void v42(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 512;
+  for (uint32_t j0 = blockIdx.x * 512 + threadIdx.x; j0 < n2; j0 += stride) {
+    const uint32_t j1 = j0 + 256;  // n2 is a multiple of 512 in this harness
+    const u64x2v* pa = reinterpret_cast<const u64x2v*>(own);
+    const u64x2v* pb = reinterpret_cast<const u64x2v*>(opp);
+    const u64x2v a0 = __builtin_nontemporal_load(pa + j0), b0 = __builtin_nontemporal_load(pb + j0);
+    const u64x2v a1 = __builtin_nontemporal_load(pa + j1), b1 = __builtin_nontemporal_load(pb + j1);
+    const uint32_t c0 = reinterpret_cast<const uint16_t*>(act)[j0], c1 = reinterpret_cast<const uint16_t*>(act)[j1];
+    uint64_t o[4], p[4], l[4]; uint16_t st[4];
+    body36(rays, a0.x, b0.x, c0 & 0xFF, true, o[0], p[0], l[0], st[0]);
+    body36(rays, a0.y, b0.y, c0 >> 8, true, o[1], p[1], l[1], st[1]);
+    body36(rays, a1.x, b1.x, c1 & 0xFF, true, o[2], p[2], l[2], st[2]);
+    body36(rays, a1.y, b1.y, c1 >> 8, true, o[3], p[3], l[3], st[3]);
+    u64x2v* qo = reinterpret_cast<u64x2v*>(oo); u64x2v* qp = reinterpret_cast<u64x2v*>(po); u64x2v* ql = reinterpret_cast<u64x2v*>(lo);
+    __builtin_nontemporal_store(u64x2v{o[0], o[1]}, qo + j0); __builtin_nontemporal_store(u64x2v{o[2], o[3]}, qo + j1);
+    __builtin_nontemporal_store(u64x2v{p[0], p[1]}, qp + j0); __builtin_nontemporal_store(u64x2v{p[2], p[3]}, qp + j1);
+    __builtin_nontemporal_store(u64x2v{l[0], l[1]}, ql + j0); __builtin_nontemporal_store(u64x2v{l[2], l[3]}, ql + j1);
+    __builtin_nontemporal_store((uint32_t)st[0] | ((uint32_t)st[1] << 16), reinterpret_cast<uint32_t*>(so) + j0);
+    __builtin_nontemporal_store((uint32_t)st[2] | ((uint32_t)st[3] << 16), reinterpret_cast<uint32_t*>(so) + j1);
+  }
+}
+// v43: v41 at 512 threads per block
+__global__ __launch_bounds__(512) void v43(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  __shared__ __align__(16) uint64_t rays[256]; if (threadIdx.x < 256) rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3); __syncthreads();
+  const uint32_t n2 = (uint32_t)(n / 2);
+  const uint32_t stride = gridDim.x * 512;
+  for (uint32_t j = blockIdx.x * 512 + threadIdx.x; j < n2; j += stride) {
+    const u64x2v a = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(own) + j);
+    const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
+    const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    uint64_t o0, p0, l0, o1, p1, l1; uint16_t s0, s1;
+    body36(rays, a.x, b.x, c & 0xFF, true, o0, p0, l0, s0);
+    body36(rays, a.y, b.y, c >> 8, true, o1, p1, l1, s1);
+    __builtin_nontemporal_store(u64x2v{o0, o1}, reinterpret_cast<u64x2v*>(oo) + j);
+    __builtin_nontemporal_store(u64x2v{p0, p1}, reinterpret_cast<u64x2v*>(po) + j);
+    __builtin_nontemporal_store(u64x2v{l0, l1}, reinterpret_cast<u64x2v*>(lo) + j);
+    __builtin_nontemporal_store((uint32_t)s0 | ((uint32_t)s1 << 16), reinterpret_cast<uint32_t*>(so) + j);
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41};
-  if (v < 0 || v > 41) return -1;
-  const int blk = v == 14 ? 64 : 256;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43};
+  if (v < 0 || v > 43) return -1;
+  const int blk = v == 14 ? 64 : (v == 43 ? 512 : 256);
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -26,7 +26,7 @@ calib_bytes = 64 << 22  # 256 MiB copied (read and written)
 rd = 2 * avg[("k_step", "FETCH_SIZE")] * 1024
 wr = avg[("k_step", "WRITE_SIZE")] * 1024
 alg = 43 * n
-out = {"kernel": "k_step (oth_step_gpu)", "positions": n, "hbm_read_bytes": rd,
+out = {"kernel": "k_step2 (oth_step_gpu)", "positions": n, "hbm_read_bytes": rd,
        "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes": alg,
        "traffic_over_algorithmic": (rd + wr) / alg,
        "calibration": {"copy_bytes_each_way": calib_bytes,

@@ -119,6 +119,32 @@ def test_step_large_batch_matches_cpu_entry_point():
     assert (o[sub] == ro).all() and (st[sub] == rs).all()
 
 
+def test_step_odd_sizes_and_unaligned_buffers():
+    """oth_step_gpu runs the paired kernel (two positions per lane, 16-byte accesses) on
+    aligned buffers and the one-per-lane kernel otherwise: odd counts (the half-live last
+    pair) and buffers offset by one element (unaligned: the fallback kernel), both
+    bit-exact against the host build of the same entry point."""
+    own, opp, act = _random_positions(1 << 17, 5)
+    for n in (1, 2, 3, 255, 257, 4097, 65537):
+        for off in (0, 1):
+            t_own, t_opp, t_act = dev(own[:n + 1]), dev(opp[:n + 1]), dev(act[:n + 1])
+            outs = [torch.zeros(n + 1, dtype=torch.int64, device="cuda") for _ in range(3)]
+            st = torch.zeros(n + 1, dtype=torch.int16, device="cuda")
+            sl = slice(off, off + n)
+            nat.check(nat.lib.oth_step_gpu(*[nat.ptr(x[sl]) for x in (t_own, t_opp, t_act)],
+                                           *[nat.ptr(x[sl]) for x in outs], nat.ptr(st[sl]), n,
+                                           nat.stream_ptr()), "oth_step_gpu")
+            torch.cuda.synchronize()
+            co, cp, cl, cs = nat.step_cpu(own[sl], opp[sl], act[sl], raise_illegal=False)
+            assert (host_u64(outs[0])[sl] == co).all(), (n, off)
+            assert (host_u64(outs[1])[sl] == cp).all(), (n, off)
+            assert (host_u64(outs[2])[sl] == cl).all(), (n, off)
+            assert (st.cpu().numpy().view(np.uint16)[sl] == cs).all(), (n, off)
+            # nothing written outside the n outputs
+            other = n if off == 0 else 0
+            assert host_u64(outs[0])[other] == 0 and st.cpu().numpy()[other] == 0, (n, off)
+
+
 def test_empty_batch_and_edge_boards():
     assert step_gpu([], [], [])[0].size == 0
     full = np.array([0xFFFFFFFFFFFFFFFF], np.uint64)
