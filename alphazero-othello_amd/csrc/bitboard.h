@@ -281,13 +281,38 @@ AZ_HD int terminal_flags(uint64_t own, uint64_t opp, uint64_t lg) {
 }
 
 // ---- wave-cooperative terminal check (device) ----------------------------------------
-// Legal placements of P against O along ONE direction d (0..3: shifts towards higher bits
-// by 1, 8, 7, 9; 4..7: the same towards lower bits), the fill of legal() split by direction
-// so that eight lanes can share one position.
-__device__ __forceinline__ uint64_t dir_moves(uint64_t P, uint64_t O, int d) {
-  const int s = (0x09070801 >> ((d & 3) * 8)) & 0xFF;
-  const uint64_t M = (d & 3) == 1 ? O : (O & kInner);
-  const bool up = d < 4;
+// The lane-dependent constants of the cooperative pass below: computed once per kernel
+// (wave_lane()) and kept in registers, so a grid-stride loop does not recompute them for
+// every position ahead of the (usually skipped) cooperative branch.
+struct WaveLane {
+  uint64_t below;  // mask of the lanes below this one
+  uint64_t bit;    // this lane's bit
+  int grp;         // lane >> 3: which pending position of a pass this lane serves
+  int s;           // shift of this lane's direction (1, 8, 7, 9)
+  bool up;         // direction towards higher bits (lane & 7 < 4)
+  bool col;        // the column direction (no wrap mask)
+};
+
+__device__ __forceinline__ WaveLane wave_lane() {
+  const int lane = __lane_id();
+  const int d = lane & 7;
+  WaveLane L;
+  L.bit = 1ull << lane;
+  L.below = L.bit - 1ull;
+  L.grp = lane >> 3;
+  L.s = (0x09070801 >> ((d & 3) * 8)) & 0xFF;
+  L.up = d < 4;
+  L.col = (d & 3) == 1;
+  return L;
+}
+
+// Legal placements of P against O along ONE direction (the lane's: shifts towards higher
+// bits by 1, 8, 7, 9 for lane & 7 = 0..3, the same towards lower bits for 4..7), the fill
+// of legal() split by direction so that eight lanes can share one position.
+__device__ __forceinline__ uint64_t dir_moves(uint64_t P, uint64_t O, const WaveLane& L) {
+  const int s = L.s;
+  const uint64_t M = L.col ? O : (O & kInner);
+  const bool up = L.up;
   uint64_t x = M & (up ? (P << s) : (P >> s));
 #pragma unroll
   for (int i = 0; i < 5; ++i) x |= M & (up ? (x << s) : (x >> s));
@@ -306,20 +331,19 @@ __device__ __forceinline__ int terminal_flags_wave(uint64_t own, uint64_t opp, u
   return -1;  // needs the cooperative pass
 }
 
-__device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp) {
-  const int lane = __lane_id();
+__device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp,
+                                                    const WaveLane& L) {
   uint64_t need = __ballot(flags < 0);
   bool other = false;
   while (need) {
-    const int grp = lane >> 3;
     uint64_t m = need;
-    for (int j = 0; j < grp && m; ++j) m &= m - 1;
-    const int src = m ? __builtin_ctzll(m) : lane;
+    for (int j = 0; j < L.grp && m; ++j) m &= m - 1;
+    const int src = m ? __builtin_ctzll(m) : 0;
     const uint64_t P = __shfl(opp, src, 64), O = __shfl(own, src, 64);
-    const uint64_t mv = m ? dir_moves(P, O, lane & 7) : 0ull;
+    const uint64_t mv = m ? dir_moves(P, O, L) : 0ull;
     const uint64_t any = __ballot(mv != 0);
-    if ((need >> lane) & 1) {
-      const int rank = popc(need & ((1ull << lane) - 1ull));
+    if (need & L.bit) {  // this lane's position is pending
+      const int rank = popc(need & L.below);
       if (rank < 8) other = ((any >> (8 * rank)) & 0xFFull) != 0;
     }
 #pragma unroll
@@ -327,6 +351,11 @@ __device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uin
   }
   if (flags >= 0) return flags;
   return other ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
+}
+
+__device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp) {
+  const WaveLane L = wave_lane();
+  return finish_terminal_wave(flags, own, opp, L);
 }
 
 struct Move {

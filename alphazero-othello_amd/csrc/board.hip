@@ -38,14 +38,15 @@ static_assert(kBlock == 64 * 4, "k_step stages one up-ray per thread");
 // with the capture set from the LDS up-ray table, the next side's legal mask, the
 // wave-cooperative terminal check (every lane of the wave must call it: uniform control
 // flow) and the status word.
-__device__ __forceinline__ void step_one(const uint64_t* rays, uint64_t o, uint64_t p, int a,
-                                         bool live, uint64_t& no, uint64_t& np, uint64_t& lg,
+__device__ __forceinline__ void step_one(const uint64_t* rays, const azb::WaveLane& L,
+                                         uint64_t o, uint64_t p, int a, bool live,
+                                         uint64_t& no, uint64_t& np, uint64_t& lg,
                                          uint16_t& st) {
   const azb::Move mv = azb::move_rays_bf(rays, o, p, a);
   const bool ok = live && !mv.illegal;
   lg = ok ? azb::legal(mv.own, mv.opp) : 0ull;
   int tf = azb::terminal_flags_wave(mv.own, mv.opp, lg, ok);
-  tf = azb::finish_terminal_wave(tf, mv.own, mv.opp);
+  tf = azb::finish_terminal_wave(tf, mv.own, mv.opp, L);
   no = mv.own;
   np = mv.opp;
   st = mv.illegal ? azb::pack_status(azb::kFlagIllegal, 0)
@@ -73,6 +74,7 @@ __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ o
   __shared__ __align__(16) uint64_t rays[64 * 4];
   rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
   __syncthreads();
+  const azb::WaveLane L = azb::wave_lane();
   const uint32_t pairs = (n + 1) / 2, full = n / 2;
   const uint32_t stride = gridDim.x * kBlock;
   const uint32_t p_pad = (pairs + kBlock - 1) / kBlock * kBlock;
@@ -94,8 +96,8 @@ __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ o
     }
     uint64_t o0, p0, l0, o1, p1, l1;
     uint16_t s0, s1;
-    step_one(rays, a.x, b.x, c & 0xFF, live0, o0, p0, l0, s0);
-    step_one(rays, a.y, b.y, c >> 8, live1, o1, p1, l1, s1);
+    step_one(rays, L, a.x, b.x, c & 0xFF, live0, o0, p0, l0, s0);
+    step_one(rays, L, a.y, b.y, c >> 8, live1, o1, p1, l1, s1);
     char* oo = reinterpret_cast<char*>(own_o) + o16;
     char* po = reinterpret_cast<char*>(opp_o) + o16;
     char* lo = reinterpret_cast<char*>(legal_o) + o16;
@@ -128,6 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
   __shared__ __align__(16) uint64_t rays[64 * 4];
   rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
   __syncthreads();
+  const azb::WaveLane L = azb::wave_lane();
   // every lane runs the same number of iterations (the terminal check is wave-cooperative)
   const uint32_t stride = gridDim.x * kBlock;
   const uint32_t n_pad = (n + kBlock - 1) / kBlock * kBlock;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
     }
     uint64_t no, np, lg;
     uint16_t st;
-    step_one(rays, o, p, a, live, no, np, lg, st);
+    step_one(rays, L, o, p, a, live, no, np, lg, st);
     if (live) {
       *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(own_o) + o8) = no;
       *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(opp_o) + o8) = np;
