@@ -91,6 +91,12 @@ int oth_d4_cpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n);
 /* ---------------- stateless board entry points: device --------------------------- */
 int oth_legal_gpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n,
                   void* stream);
+/* oth_step_cpu on device, asynchronous on `stream` (device pointers, n < 2^28).  With
+ * 16-byte aligned own/opp/own_o/opp_o/legal_o, a 2-byte aligned act and a 4-byte aligned
+ * status_o (any torch allocation) it runs two positions per lane with 16-byte
+ * non-temporal accesses; other alignments take a one-position-per-lane kernel with the
+ * same results.  Illegal placements are reported in status (kFlagIllegal), not as an
+ * error code. */
 int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
                  uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
                  int64_t n, void* stream);
