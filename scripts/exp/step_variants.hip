@@ -775,11 +775,116 @@ __global__ __launch_bounds__(512) void v43(const uint64_t* own, const uint64_t* 
   }
 }
 
+// v44: product k_step2 body (lane constants hoisted); v45: the same with the two positions'
+// phases separated (both moves, both legal masks, then both terminal checks) for ILP
+template <bool SPLIT>
+__device__ __forceinline__ void pair44(const uint64_t* rays, const azb::WaveLane& L, u64x2v a, u64x2v b, uint32_t c, bool live,
+  uint64_t* r) {
+  if (SPLIT) {
+    const azb::Move m0 = azb::move_rays_bf(rays, a.x, b.x, c & 0xFF);
+    const azb::Move m1 = azb::move_rays_bf(rays, a.y, b.y, c >> 8);
+    const bool ok0 = live && !m0.illegal, ok1 = live && !m1.illegal;
+    const uint64_t l0 = ok0 ? azb::legal(m0.own, m0.opp) : 0ull;
+    const uint64_t l1 = ok1 ? azb::legal(m1.own, m1.opp) : 0ull;
+    int t0 = azb::terminal_flags_wave(m0.own, m0.opp, l0, ok0);
+    int t1 = azb::terminal_flags_wave(m1.own, m1.opp, l1, ok1);
+    t0 = azb::finish_terminal_wave(t0, m0.own, m0.opp, L);
+    t1 = azb::finish_terminal_wave(t1, m1.own, m1.opp, L);
+    r[0] = m0.own; r[1] = m1.own; r[2] = m0.opp; r[3] = m1.opp; r[4] = l0; r[5] = l1;
+    const uint16_t s0 = m0.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m0.flags | t0, azb::popc(m0.own) - azb::popc(m0.opp));
+    const uint16_t s1 = m1.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m1.flags | t1, azb::popc(m1.own) - azb::popc(m1.opp));
+    r[6] = (uint32_t)s0 | ((uint32_t)s1 << 16);
+  } else {
+    for (int k = 0; k < 2; ++k) {
+      const azb::Move m = azb::move_rays_bf(rays, k ? a.y : a.x, k ? b.y : b.x, k ? (c >> 8) : (c & 0xFF));
+      const bool ok = live && !m.illegal;
+      const uint64_t lg = ok ? azb::legal(m.own, m.opp) : 0ull;
+      int t = azb::terminal_flags_wave(m.own, m.opp, lg, ok);
+      t = azb::finish_terminal_wave(t, m.own, m.opp, L);
+      r[k] = m.own; r[2 + k] = m.opp; r[4 + k] = lg;
+      const uint16_t s = m.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m.flags | t, azb::popc(m.own) - azb::popc(m.opp));
+      r[6] = k ? (r[6] | ((uint32_t)s << 16)) : s;
+    }
+  }
+}
+template <bool SPLIT>
+__device__ __forceinline__ void k44(const uint64_t* rays, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  const azb::WaveLane L = azb::wave_lane();
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n2; j += stride) {
+    const u64x2v a = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(own) + j);
+    const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
+    const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    uint64_t r[7];
+    pair44<SPLIT>(rays, L, a, b, c, true, r);
+    __builtin_nontemporal_store(u64x2v{r[0], r[1]}, reinterpret_cast<u64x2v*>(oo) + j);
+    __builtin_nontemporal_store(u64x2v{r[2], r[3]}, reinterpret_cast<u64x2v*>(po) + j);
+    __builtin_nontemporal_store(u64x2v{r[4], r[5]}, reinterpret_cast<u64x2v*>(lo) + j);
+    __builtin_nontemporal_store((uint32_t)r[6], reinterpret_cast<uint32_t*>(so) + j);
+  }
+}
+__global__ __launch_bounds__(256) void v44(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k44<false>(rays, own, opp, act, oo, po, lo, so, n);
+}
+__global__ __launch_bounds__(256) void v45(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k44<true>(rays, own, opp, act, oo, po, lo, so, n);
+}
+
+// v46 / v47: sensitivity probes on the product body — 20 extra `s_nop 0` per position
+// (are the hazard pads after inline-asm shifts free?) / 20 extra dependent-free VALU per
+// position (what does one VALU cost?)
+template <int PROBE>
+__device__ __forceinline__ void k46(const uint64_t* rays, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  const azb::WaveLane L = azb::wave_lane();
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n2; j += stride) {
+    const u64x2v a = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(own) + j);
+    const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
+    const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    uint64_t r[7];
+    pair44<false>(rays, L, a, b, c, true, r);
+    if (PROBE == 1) {
+#pragma unroll
+      for (int k = 0; k < 40; ++k) asm volatile("s_nop 0");
+    } else if (PROBE == 2) {
+      uint32_t x0 = (uint32_t)r[0], x1 = (uint32_t)r[1], x2 = (uint32_t)r[2], x3 = (uint32_t)r[3];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        asm volatile("v_xor_b32 %0, %0, %1\n\tv_xor_b32 %1, %1, %0\n\tv_xor_b32 %2, %2, %3\n\tv_xor_b32 %3, %3, %2"
+                     : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+      }
+      r[6] ^= (x0 ^ x1 ^ x2 ^ x3) & 0x80000000u & (uint32_t)(r[4] >> 63);  // keep them live
+    }
+    __builtin_nontemporal_store(u64x2v{r[0], r[1]}, reinterpret_cast<u64x2v*>(oo) + j);
+    __builtin_nontemporal_store(u64x2v{r[2], r[3]}, reinterpret_cast<u64x2v*>(po) + j);
+    __builtin_nontemporal_store(u64x2v{r[4], r[5]}, reinterpret_cast<u64x2v*>(lo) + j);
+    __builtin_nontemporal_store((uint32_t)r[6], reinterpret_cast<uint32_t*>(so) + j);
+  }
+}
+__global__ __launch_bounds__(256) void v46(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k46<1>(rays, own, opp, act, oo, po, lo, so, n);
+}
+__global__ __launch_bounds__(256) void v47(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k46<2>(rays, own, opp, act, oo, po, lo, so, n);
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43};
-  if (v < 0 || v > 43) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47};
+  if (v < 0 || v > 47) return -1;
   const int blk = v == 14 ? 64 : (v == 43 ? 512 : 256);
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
