@@ -33,9 +33,10 @@ Also measured in the same run:
                 position (read own, opp, act = 17; write own', opp', legal, status = 26),
                 HIP events on the launch stream; traffic = HBM bytes from rocprofv3 PMC
                 (profiles/oth_step_traffic.json), or null.
-  cpu_baseline  the oracle's restatement of the reference self-play (oracle/selfplay.py:
+  cpu_baseline  the oracle's restatement of the reference self-play (oracle/mcts.py:
                 sequential MCTS, batch-1 torch-CPU inference of the same net, the C board
-                oracle) on 1 host core for a bounded sample of moves.
+                oracle) in --cpu-workers single-threaded processes (default 8) for a
+                bounded sample of moves each, games/s summed.
 """
 import argparse
 import json
@@ -97,6 +98,8 @@ def parse():
                          "kernel tracer crashes on multi-step captures)")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-workers", type=int, default=8,
+                    help="host cores (one single-threaded process each) for cpu_baseline")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-kernel", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "oth_step_traffic.json"))
@@ -259,7 +262,7 @@ def conv_roofline(sp, device, n_boards):
     return out
 
 
-def cpu_baseline(net, seconds):
+def cpu_baseline(net_kind, sims, seconds, seed=0):
     """The oracle's restatement of one_self_play (reference algorithm, sequential MCTS,
     batch-1 torch-CPU inference, C board oracle), timed for a bounded sample of moves of one
     game on one core; games/s = 1 / (seconds per move x plies per game)."""
@@ -267,7 +270,7 @@ def cpu_baseline(net, seconds):
     from oracle.mcts import SeqMCTS
 
     torch.set_num_threads(1)
-    cpu_net = net.cpu().eval()
+    cpu_net = make_net(net_kind).cpu().eval()
 
     def evaluate(own, opp, player):
         s = ob.to_state(own, opp, player)
@@ -277,9 +280,9 @@ def cpu_baseline(net, seconds):
             p = torch.softmax(logits, -1)
         return p[0].numpy(), float(v[0, 0])
 
-    np.random.seed(0)
+    np.random.seed(seed)
     a = SELFPLAY_ARGS
-    m = SeqMCTS(a["c_puct"], a["num_simulations"], evaluate, dirichlet_alpha=a["dirichlet_alpha"],
+    m = SeqMCTS(a["c_puct"], sims, evaluate, dirichlet_alpha=a["dirichlet_alpha"],
                 dirichlet_epsilon=a["dirichlet_epsilon"])
     game = ob.OracleGame()
     state, player = game.get_initial_state(), 1
@@ -296,12 +299,38 @@ def cpu_baseline(net, seconds):
             break
         player = -player
     dt = time.perf_counter() - t0
-    per_move = dt / moves
-    return {"value": 1.0 / (per_move * REF_PLIES_PER_GAME), "unit": "games/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{moves} moves of one self-play game at 400 sims, AlphaZeroNet(5,128) "
-                      f"fp32 batch-1 torch-CPU, oracle/mcts.py SeqMCTS; {dt:.1f}s; "
-                      f"games/s = 1/(s_per_move x {REF_PLIES_PER_GAME:.0f} plies)"}
+    return {"moves": moves, "seconds": dt,
+            "games_per_s": 1.0 / (dt / moves * REF_PLIES_PER_GAME)}
+
+
+def cpu_baseline_pool(net_kind, sims, seconds, workers):
+    """cpu_baseline on `workers` host cores at once, one process each (started before any
+    GPU work of theirs could exist: they hide the GPUs), like the reference's spawn-pool
+    self-play workers (train.py:220-222); games/s summed over the workers."""
+    import subprocess
+
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                               net_kind, str(sims), str(seconds), str(w)],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env)
+             for w in range(workers)]
+    outs = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=seconds * 10 + 120)
+        if pr.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker failed ({pr.returncode})")
+        outs.append(json.loads(out.decode().strip().splitlines()[-1]))
+    moves = sum(o["moves"] for o in outs)
+    net_name = "AlphaZeroNet(5,128)" if net_kind == "az5x128" else "FastOthelloNet"
+    return {"value": float(sum(o["games_per_s"] for o in outs)), "unit": "games/s",
+            "cores": workers, "kind": "port",
+            "sample": f"{workers} single-threaded worker processes, each the opening moves "
+                      f"of one self-play game (seeds 0..{workers - 1}; {moves} moves in all) "
+                      f"at {sims} sims for {seconds:.0f} s; {net_name} fp32 batch-1 torch-CPU, "
+                      f"oracle/mcts.py SeqMCTS; per worker games/s = 1/(s_per_move x "
+                      f"{REF_PLIES_PER_GAME:.0f} plies), summed",
+            "per_worker_games_per_s": [round(o["games_per_s"], 5) for o in outs]}
 
 
 def main():
@@ -450,8 +479,7 @@ def main():
             and getattr(sp.net, "conv_impl", "") == "hip":
         result["roofline_conv"] = conv_roofline(sp, device, a.games)
     if rank == 0 and world == 1 and not a.skip_cpu:
-        result["cpu_baseline"] = cpu_baseline(make_net(a.net), a.cpu_seconds)
-        result["cpu_baseline"]["cores"] = 1
+        result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds, a.cpu_workers)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
@@ -459,4 +487,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":  # cpu_baseline_pool's workers
+        print(json.dumps(cpu_baseline(sys.argv[2], int(sys.argv[3]), float(sys.argv[4]),
+                                      int(sys.argv[5]))), flush=True)
+    else:
+        main()
