@@ -215,3 +215,23 @@ def test_augment_tables_match_reference_get_random_symmetry():
         p = nat.d4_cpu(d["neg"][i:i + 1], int(sym[i]))[0]
         plane = ((o & w) != 0).astype(np.float32) - ((p & w) != 0).astype(np.float32)
         assert np.array_equal(plane.reshape(1, 8, 8), d["out_state"][i])
+
+
+def test_bench_kernel_inputs_are_legal_playouts():
+    """bench.py's kernel-roofline inputs (seeded random playouts, one legal
+    action each, or the pass when there is none) are reproducible, every action is legal
+    for its position, and the oracle steps all of them without an illegal placement."""
+    import bench
+    from oracle import board as ob
+
+    own, opp, act = bench.playout_positions(games=64)
+    own2, opp2, act2 = bench.playout_positions(games=64)
+    assert (own == own2).all() and (opp == opp2).all() and (act == act2).all()
+    assert len(own) > 64 * 50  # games run to (near) the end
+    lg = ob.legal_batch(own, opp)
+    passes = act == 64
+    assert (passes == (lg == 0)).all()
+    placed = ~passes
+    assert ((lg[placed] >> act[placed].astype(np.uint64)) & np.uint64(1)).all()
+    _, _, _, _, bad = ob.step_batch(own, opp, act)
+    assert bad == -1
