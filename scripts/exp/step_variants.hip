@@ -880,11 +880,40 @@ __global__ __launch_bounds__(256) void v47(const uint64_t* own, const uint64_t* 
   k46<2>(rays, own, opp, act, oo, po, lo, so, n);
 }
 
+// v48: probe — v44 without the cooperative terminal pass (terminal flags wrong for real
+// passes): what the rare pass costs on this corpus
+__global__ __launch_bounds__(256) void v48(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n2; j += stride) {
+    const u64x2v a = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(own) + j);
+    const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
+    const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    uint64_t r[7];
+    for (int k = 0; k < 2; ++k) {
+      const azb::Move m = azb::move_rays_bf(rays, k ? a.y : a.x, k ? b.y : b.x, k ? (c >> 8) : (c & 0xFF));
+      const bool ok = !m.illegal;
+      const uint64_t lg = ok ? azb::legal(m.own, m.opp) : 0ull;
+      int t = azb::terminal_flags_wave(m.own, m.opp, lg, ok);
+      t = t < 0 ? azb::kFlagNoPlace : t;
+      r[k] = m.own; r[2 + k] = m.opp; r[4 + k] = lg;
+      const uint16_t s = m.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m.flags | t, azb::popc(m.own) - azb::popc(m.opp));
+      r[6] = k ? (r[6] | ((uint32_t)s << 16)) : s;
+    }
+    __builtin_nontemporal_store(u64x2v{r[0], r[1]}, reinterpret_cast<u64x2v*>(oo) + j);
+    __builtin_nontemporal_store(u64x2v{r[2], r[3]}, reinterpret_cast<u64x2v*>(po) + j);
+    __builtin_nontemporal_store(u64x2v{r[4], r[5]}, reinterpret_cast<u64x2v*>(lo) + j);
+    __builtin_nontemporal_store((uint32_t)r[6], reinterpret_cast<uint32_t*>(so) + j);
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47};
-  if (v < 0 || v > 47) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47, v48};
+  if (v < 0 || v > 48) return -1;
   const int blk = v == 14 ? 64 : (v == 43 ? 512 : 256);
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
