@@ -331,9 +331,22 @@ __device__ __forceinline__ int terminal_flags_wave(uint64_t own, uint64_t opp, u
   return -1;  // needs the cooperative pass
 }
 
+// PRE: a wave with pending lanes first tries the other side's horizontal placements
+// (the carry pair of legal(), ~20 VALU once for the wave); only lanes still undecided
+// enter the cooperative fill of all eight directions (~70 VALU per pass).
+template <int PRE = 1>
 __device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp,
                                                     const WaveLane& L) {
   uint64_t need = __ballot(flags < 0);
+  if (PRE && need) {
+    if (flags < 0) {  // placements of opp against own along the rows (legal(opp, own))
+      uint64_t m = moves_row_up(opp, own & kInner) |
+                   rev64(moves_row_up(rev64(opp), rev64(own) & kInner));
+      if (PRE > 1) m |= moves_dir<8>(opp, own);  // and the columns
+      if (m & ~(own | opp)) flags = kFlagNoPlace;
+    }
+    need = __ballot(flags < 0);
+  }
   bool other = false;
   while (need) {
     uint64_t m = need;
@@ -355,7 +368,7 @@ __device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uin
 
 __device__ __forceinline__ int finish_terminal_wave(int flags, uint64_t own, uint64_t opp) {
   const WaveLane L = wave_lane();
-  return finish_terminal_wave(flags, own, opp, L);
+  return finish_terminal_wave<1>(flags, own, opp, L);
 }
 
 struct Move {

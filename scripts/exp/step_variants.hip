@@ -777,7 +777,7 @@ __global__ __launch_bounds__(512) void v43(const uint64_t* own, const uint64_t* 
 
 // v44: product k_step2 body (lane constants hoisted); v45: the same with the two positions'
 // phases separated (both moves, both legal masks, then both terminal checks) for ILP
-template <bool SPLIT>
+template <bool SPLIT, int PRE = 1>
 __device__ __forceinline__ void pair44(const uint64_t* rays, const azb::WaveLane& L, u64x2v a, u64x2v b, uint32_t c, bool live,
   uint64_t* r) {
   if (SPLIT) {
@@ -800,14 +800,14 @@ __device__ __forceinline__ void pair44(const uint64_t* rays, const azb::WaveLane
       const bool ok = live && !m.illegal;
       const uint64_t lg = ok ? azb::legal(m.own, m.opp) : 0ull;
       int t = azb::terminal_flags_wave(m.own, m.opp, lg, ok);
-      t = azb::finish_terminal_wave(t, m.own, m.opp, L);
+      t = azb::finish_terminal_wave<PRE>(t, m.own, m.opp, L);
       r[k] = m.own; r[2 + k] = m.opp; r[4 + k] = lg;
       const uint16_t s = m.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m.flags | t, azb::popc(m.own) - azb::popc(m.opp));
       r[6] = k ? (r[6] | ((uint32_t)s << 16)) : s;
     }
   }
 }
-template <bool SPLIT>
+template <bool SPLIT, int PRE = 1>
 __device__ __forceinline__ void k44(const uint64_t* rays, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
   const azb::WaveLane L = azb::wave_lane();
@@ -818,7 +818,7 @@ __device__ __forceinline__ void k44(const uint64_t* rays, const uint64_t* own, c
     const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
     const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
     uint64_t r[7];
-    pair44<SPLIT>(rays, L, a, b, c, true, r);
+    pair44<SPLIT, PRE>(rays, L, a, b, c, true, r);
     __builtin_nontemporal_store(u64x2v{r[0], r[1]}, reinterpret_cast<u64x2v*>(oo) + j);
     __builtin_nontemporal_store(u64x2v{r[2], r[3]}, reinterpret_cast<u64x2v*>(po) + j);
     __builtin_nontemporal_store(u64x2v{r[4], r[5]}, reinterpret_cast<u64x2v*>(lo) + j);
@@ -909,11 +909,25 @@ __global__ __launch_bounds__(256) void v48(const uint64_t* own, const uint64_t* 
   }
 }
 
+// v49: v44 without the row pre-test of the cooperative terminal pass (A/B for it)
+__global__ __launch_bounds__(256) void v49(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k44<false, 0>(rays, own, opp, act, oo, po, lo, so, n);
+}
+
+// v50: v44 with the row + column pre-test
+__global__ __launch_bounds__(256) void v50(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n) {
+  RAYS
+  k44<false, 2>(rays, own, opp, act, oo, po, lo, so, n);
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47, v48};
-  if (v < 0 || v > 48) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50};
+  if (v < 0 || v > 50) return -1;
   const int blk = v == 14 ? 64 : (v == 43 ? 512 : 256);
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
