@@ -923,11 +923,86 @@ __global__ __launch_bounds__(256) void v50(const uint64_t* own, const uint64_t* 
   k44<false, 2>(rays, own, opp, act, oo, po, lo, so, n);
 }
 
+// The terminal check of two positions per lane (a lane's pair, f0/f1 from
+// terminal_flags_wave) in ONE sequence of cooperative passes: the pending positions of both
+// halves form one list (position 0's pending lanes, then position 1's), eight per pass.
+namespace azb {
+template <int PRE = 1>
+__device__ __forceinline__ void finish_terminal_wave2(int& f0, uint64_t own0, uint64_t opp0,
+                                                      int& f1, uint64_t own1, uint64_t opp1,
+                                                      const WaveLane& L) {
+  uint64_t n0 = __ballot(f0 < 0), n1 = __ballot(f1 < 0);
+  if (!(n0 | n1)) return;
+  if (PRE) {
+    if (f0 < 0) {
+      const uint64_t m = moves_row_up(opp0, own0 & kInner) |
+                         rev64(moves_row_up(rev64(opp0), rev64(own0) & kInner));
+      if (m & ~(own0 | opp0)) f0 = kFlagNoPlace;
+    }
+    if (f1 < 0) {
+      const uint64_t m = moves_row_up(opp1, own1 & kInner) |
+                         rev64(moves_row_up(rev64(opp1), rev64(own1) & kInner));
+      if (m & ~(own1 | opp1)) f1 = kFlagNoPlace;
+    }
+    n0 = __ballot(f0 < 0);
+    n1 = __ballot(f1 < 0);
+  }
+  const int c0 = popc(n0), total = c0 + popc(n1);
+  const int r0 = popc(n0 & L.below), r1 = c0 + popc(n1 & L.below);
+  bool o0 = false, o1 = false;
+  for (int base = 0; base < total; base += 8) {
+    const int item = base + L.grp;
+    const bool second = item >= c0;
+    uint64_t m = item < total ? (second ? n1 : n0) : 0ull;
+    const int k = second ? item - c0 : item;
+    for (int j = 0; j < k && m; ++j) m &= m - 1;
+    const int src = m ? __builtin_ctzll(m) : 0;
+    const uint64_t P0 = __shfl(opp0, src, 64), O0 = __shfl(own0, src, 64);
+    const uint64_t P1 = __shfl(opp1, src, 64), O1 = __shfl(own1, src, 64);
+    const uint64_t mv = m ? dir_moves(second ? P1 : P0, second ? O1 : O0, L) : 0ull;
+    const uint64_t any = __ballot(mv != 0);
+    if (f0 < 0 && r0 >= base && r0 < base + 8) o0 = ((any >> (8 * (r0 - base))) & 0xFFull) != 0;
+    if (f1 < 0 && r1 >= base && r1 < base + 8) o1 = ((any >> (8 * (r1 - base))) & 0xFFull) != 0;
+  }
+  if (f0 < 0) f0 = o0 ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
+  if (f1 < 0) f1 = o1 ? kFlagNoPlace : (kFlagNoPlace | kFlagTerminal);
+}
+}  // namespace azb
+
+// v51: v45 (phases split) with one merged cooperative terminal pass for the pair
+__global__ __launch_bounds__(256) void v51(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+  uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n_) {
+  RAYS
+  const azb::WaveLane L = azb::wave_lane();
+  const uint32_t n2 = (uint32_t)(n_ / 2);
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n2; j += stride) {
+    const u64x2v a = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(own) + j);
+    const u64x2v b = __builtin_nontemporal_load(reinterpret_cast<const u64x2v*>(opp) + j);
+    const uint32_t c = reinterpret_cast<const uint16_t*>(act)[j];
+    const azb::Move m0 = azb::move_rays_bf(rays, a.x, b.x, c & 0xFF);
+    const bool ok0 = !m0.illegal;
+    const uint64_t l0 = ok0 ? azb::legal(m0.own, m0.opp) : 0ull;
+    const azb::Move m1 = azb::move_rays_bf(rays, a.y, b.y, c >> 8);
+    const bool ok1 = !m1.illegal;
+    const uint64_t l1 = ok1 ? azb::legal(m1.own, m1.opp) : 0ull;
+    int t0 = azb::terminal_flags_wave(m0.own, m0.opp, l0, ok0);
+    int t1 = azb::terminal_flags_wave(m1.own, m1.opp, l1, ok1);
+    azb::finish_terminal_wave2(t0, m0.own, m0.opp, t1, m1.own, m1.opp, L);
+    const uint16_t s0 = m0.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m0.flags | t0, azb::popc(m0.own) - azb::popc(m0.opp));
+    const uint16_t s1 = m1.illegal ? azb::pack_status(azb::kFlagIllegal, 0) : azb::pack_status(m1.flags | t1, azb::popc(m1.own) - azb::popc(m1.opp));
+    __builtin_nontemporal_store(u64x2v{m0.own, m1.own}, reinterpret_cast<u64x2v*>(oo) + j);
+    __builtin_nontemporal_store(u64x2v{m0.opp, m1.opp}, reinterpret_cast<u64x2v*>(po) + j);
+    __builtin_nontemporal_store(u64x2v{l0, l1}, reinterpret_cast<u64x2v*>(lo) + j);
+    __builtin_nontemporal_store((uint32_t)s0 | ((uint32_t)s1 << 16), reinterpret_cast<uint32_t*>(so) + j);
+  }
+}
+
 extern "C" int run_variant(int v, const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   uint64_t* oo, uint64_t* po, uint64_t* lo, uint16_t* so, int64_t n, int grid, void* stream) {
   void (*ks[])(const uint64_t*, const uint64_t*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint16_t*, int64_t) =
-    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50};
-  if (v < 0 || v > 50) return -1;
+    {v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v0, v16, v17, v18, v19, v20, v21, v22, v23, v24, v25, v26, v27, v28, v29, v30, v31, v32, v33, v34, v35, v36, v37, v38, v39, v40, v41, v42, v43, v44, v45, v46, v47, v48, v49, v50, v51};
+  if (v < 0 || v > 51) return -1;
   const int blk = v == 14 ? 64 : (v == 43 ? 512 : 256);
   hipLaunchKernelGGL(ks[v], dim3(v == 14 ? grid * 4 : grid), dim3(blk), 0, (hipStream_t)stream, own, opp, act, oo, po, lo, so, n);
   return hipGetLastError() == hipSuccess ? 0 : -3;
