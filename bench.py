@@ -244,9 +244,16 @@ def conv_roofline(sp, device, n_boards):
     ms = launch_ms(lambda: fn(*args), 100)
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
+    traffic = None  # HBM bytes per launch, PMC (scripts/pmc_conv.sh), for the Winograd form
+    tj = os.path.join(ROOT, "profiles", "conv_traffic.json")
+    if "wino" in kname and conv.precision == "split3" and C == 128 and os.path.exists(tj):
+        try:
+            traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
     out = {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
            "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-           "frac": round(achieved / peak, 4), "traffic": None, "boards": n_boards,
+           "frac": round(achieved / peak, 4), "traffic": traffic, "boards": n_boards,
            "channels": C, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
            "mfma_flop_per_algorithmic_flop": round(mult, 4),
            "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1)}
