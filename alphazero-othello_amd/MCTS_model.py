@@ -175,7 +175,13 @@ class _EngineSearch:
         if isinstance(self.policy, torch.nn.Module) and hasattr(self.policy, "evaluate_planes"):
             import copy
 
-            self.dev_policy = copy.deepcopy(self.policy).to(self.engine.device).eval()
+            from Models import AlphaZeroNet, FastOthelloNet, inference_copy
+
+            if isinstance(self.policy, (AlphaZeroNet, FastOthelloNet)):
+                # the same fused HIP inference copy the batched engine runs (fp32-accurate)
+                self.dev_policy = inference_copy(self.policy, self.engine.device)
+            else:
+                self.dev_policy = copy.deepcopy(self.policy).to(self.engine.device).eval()
 
     def reset(self):
         self.has_root = False
@@ -187,14 +193,44 @@ class _EngineSearch:
         e = self.engine
         if self.dev_policy is not None:
             with torch.no_grad():
-                pr, va = self.dev_policy.evaluate_planes(e.nn_in)
-            e.priors.copy_(pr)
-            e.values.copy_(va)
+                if hasattr(self.dev_policy, "evaluate_into"):
+                    self.dev_policy.evaluate_into(e.nn_in, e.priors, e.values)
+                else:
+                    pr, va = self.dev_policy.evaluate_planes(e.nn_in)
+                    e.priors.copy_(pr)
+                    e.values.copy_(va)
             return
         canon = np.rint(e.nn_in[0].cpu().numpy()).astype(np.int8).reshape(8, 8)
         priors, value = self.policy.inference(canon, 1)
         e.priors[0].copy_(torch.from_numpy(np.asarray(priors, np.float32).reshape(65)))
         e.values[0] = float(value)
+
+    def _device_iteration(self):
+        e = self.engine
+        e.select()
+        self._evaluate()
+        e.expand()
+
+    def _run_on_device(self, n):
+        """n select -> net -> expand iterations with no host synchronisation, replayed from
+        one captured HIP graph of a single iteration (captured on first use)."""
+        import torch
+
+        if getattr(self, "_graph", None) is None:
+            s = torch.cuda.Stream(device=self.engine.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.no_grad(), torch.cuda.stream(s):
+                # the first iteration runs eagerly (it also warms the kernels up); capturing
+                # does not execute the captured work
+                self._device_iteration()
+            torch.cuda.current_stream().wait_stream(s)
+            n -= 1
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                self._device_iteration()
+            self._graph = g
+        for _ in range(n):
+            self._graph.replay()
 
     def search(self, init_state, init_player, temp):
         self._ensure()
@@ -214,18 +250,27 @@ class _EngineSearch:
             # the root will be expanded inside this call: Dirichlet noise (MCTS_model.py:340)
             e.inject(noise=np.random.dirichlet([self.alpha] * 65).reshape(1, 1, 65))
         e.begin_search(0, self.args["num_simulations"])
+        if self.dev_policy is not None:
+            # every select either hands out a leaf or finishes the search (its descent budget
+            # covers all simulations), so sims + 1 iterations (the root expansion included)
+            # complete it: no per-simulation host round trip
+            self._run_on_device(self.args["num_simulations"] + 1)
         guard = 0
         while True:
             e.select()
             leaf = int(e.leaf[0].item())
             if leaf < 0:
-                if e.game_info()["status"][0] != 1 or guard > 1000:
+                info = e.game_info()
+                if info["status"][0] != 1 or guard > 1000:
                     break
                 guard += 1
                 continue
             if self.policy is not None:
                 self._evaluate()
             e.expand()
+        if info["overflow"][0]:
+            # an expansion was skipped (engine.hip k_expand): no longer the reference's search
+            raise RuntimeError("MCTS node arena overflow: the search diverged from the reference")
         _, counts, _ = e.root_policy(0, 1.0)
         tree = self.root_tree()
         return _pi_from_counts(counts.astype(np.float32), temp,

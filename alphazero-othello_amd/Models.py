@@ -229,8 +229,8 @@ def default_conv_algo(precision, channels):
     where it measured faster (split3, 128 channels: profiles/r01_conv_mx.jsonl), "direct"
     (csrc/conv16.hip) elsewhere; AZ_CONV_ALGO=direct|wino overrides."""
     env = os.environ.get("AZ_CONV_ALGO")
-    if env in ("direct", "wino"):
-        return env
+    if env in ("direct", "wino", "wino4"):
+        return "wino" if env == "wino4" and channels != 128 else env
     return "wino" if precision == "split3" and channels == 128 else "direct"
 
 
@@ -253,6 +253,8 @@ class _HipConv3x3(nn.Module):
         self.channels = co
         self.precision = precision
         self.algo = "direct" if precision == "fp32" else (algo or default_conv_algo(precision, co))
+        if self.algo == "wino4" and co != 128:  # the 4-board form is built for 128 channels
+            self.algo = "wino"
         w9 = w.float().permute(2, 3, 0, 1).reshape(9, co, ci).contiguous()
         self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
         if precision == "fp32":
@@ -260,9 +262,10 @@ class _HipConv3x3(nn.Module):
         else:
             self.mode = self.MODES[precision]
             planes = 3 if precision == "split3" else 1
-            taps = 16 if self.algo == "wino" else 9
+            wino = self.algo in ("wino", "wino4")
+            taps = 16 if wino else 9
             wq = torch.empty(taps * co * ci * planes, dtype=torch.int16, device=w.device)
-            prep = nat.lib.az_conv3x3_wino_prep_gpu if self.algo == "wino" else nat.lib.az_conv3x3_mx_prep_gpu
+            prep = nat.lib.az_conv3x3_wino_prep_gpu if wino else nat.lib.az_conv3x3_mx_prep_gpu
             nat.check(prep(nat.ptr(w9), nat.ptr(wq), co, self.mode, nat.stream_ptr()),
                       "conv3x3 weight prep")
             self.wq = nn.Parameter(wq, requires_grad=False)
@@ -281,10 +284,12 @@ class _HipConv3x3(nn.Module):
                                         nat.stream_ptr())
             nat.check(rc, "az_conv3x3_gpu")
         else:
-            fn = nat.lib.az_conv3x3_wino_gpu if self.algo == "wino" else nat.lib.az_conv3x3_mx_gpu
-            rc = fn(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp, nat.ptr(y), x.shape[0],
-                    self.channels, int(relu), self.mode, nat.stream_ptr())
-            nat.check(rc, "az_conv3x3_wino_gpu" if self.algo == "wino" else "az_conv3x3_mx_gpu")
+            name = {"wino": "az_conv3x3_wino_gpu", "wino4": "az_conv3x3_wino4_gpu",
+                    "direct": "az_conv3x3_mx_gpu"}[self.algo]
+            rc = getattr(nat.lib, name)(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp,
+                                        nat.ptr(y), x.shape[0], self.channels, int(relu),
+                                        self.mode, nat.stream_ptr())
+            nat.check(rc, name)
         return y
 
     def forward_stem(self, planes, stem, role, x=None):

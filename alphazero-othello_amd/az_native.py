@@ -99,7 +99,7 @@ SIGNATURES = {
     "az_root_stats": [_P, _P, _P, _P],
     "az_reroot_slots": [_P, _P, _P, _P],
     "az_game_info": [_P, _P, _P, _P, _P, _P, _P, _P],
-    "az_export_tree": [_P, _I32, _I32] + [_P] * 13,
+    "az_export_tree": [_P, _I32, _I32] + [_P] * 14,
     "az_export_trajectory": [_P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
     "az_samples": [_P, _P, _P, _P, _P, _P, _P, _P],
     "az_copy_samples": [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
@@ -112,6 +112,7 @@ SIGNATURES = {
     "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_wino_prep_gpu": [_P, _P, _I32, _I32, _P],
     "az_conv3x3_wino_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
+    "az_conv3x3_wino4_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_trunk_wino_gpu": [_P] * 7 + [_I32] * 4 + [_P],
     "az_heads_az_gpu": [_P] * 11 + [_I32, _I32, _P],
     "az_conv3x3_mx_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P],
@@ -132,8 +133,9 @@ def _load():
             f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` (build()) "
             "or `python alphazero-othello_amd/az_build.py`; there is no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
-    lib.az_last_error.argtypes = []
-    lib.az_last_error.restype = ctypes.c_char_p
+    for name in ("az_last_error", "az_build_id"):
+        getattr(lib, name).argtypes = []
+        getattr(lib, name).restype = ctypes.c_char_p
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -142,6 +144,11 @@ def _load():
 
 
 lib = _load()
+
+
+def build_id():
+    """sha256 of the sources the loaded library was compiled from (az_build.source_hash)."""
+    return lib.az_build_id().decode()
 
 
 def last_error():

@@ -201,6 +201,13 @@ extern "C" {
 const char* az_last_error(void) { return azc::g_last_error.c_str(); }
 int az_abi_version(void) { return AZ_ABI_VERSION; }
 
+#ifndef AZ_BUILD_ID
+#error "AZ_BUILD_ID must be defined by the build (az_build.py: sha256 of the sources)"
+#endif
+// the marker prefix lets az_build.py find the id in the .so without loading it
+static const char kBuildIdTag[] = "AZ_BUILD_ID=" AZ_BUILD_ID;
+const char* az_build_id(void) { return kBuildIdTag + 12; }
+
 int oth_legal_cpu(const uint64_t* own, const uint64_t* opp, uint64_t* legal_o, int64_t n) {
   AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_legal_cpu: n=%lld < 0", (long long)n);
   AZ_REQUIRE(n == 0 || (own && opp && legal_o), AZ_ERR_ARG, "oth_legal_cpu: null buffer");

@@ -883,12 +883,21 @@ __device__ void finish_game(const Params& p, int g, int n_plies, int winner, int
     __syncthreads();
   }
   if (tid == 0) {
-    unsigned long long base = atomicAdd(&p.ctr->samples_n, (unsigned long long)n_plies);
-    s_ok = (int64_t)(base + n_plies) <= p.s.cap;
-    if (!s_ok) {
-      atomicAdd(&p.ctr->samples_n, (unsigned long long)(-(long long)n_plies));
-      atomicAdd(&p.ctr->samples_dropped, (unsigned long long)n_plies);
+    // reserve [base, base + n_plies) only if it fits: the counter advances by a successful
+    // compare-and-swap and is never rolled back, so a rejected game cannot lower it under
+    // rows another workgroup has already reserved
+    unsigned long long base = __hip_atomic_load(&p.ctr->samples_n, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    s_ok = 0;
+    while ((int64_t)(base + n_plies) <= p.s.cap) {
+      const unsigned long long prev = atomicCAS(&p.ctr->samples_n, base, base + n_plies);
+      if (prev == base) {
+        s_ok = 1;
+        break;
+      }
+      base = prev;
     }
+    if (!s_ok) atomicAdd(&p.ctr->samples_dropped, (unsigned long long)n_plies);
     s_base = base;
     if (s_ok) {
       double g_next = 0.0;

@@ -344,4 +344,20 @@ class BatchedSelfPlay:
             self.step(check_every)
             steps += check_every
             done = e.counters()["games_finished"]
+        check_complete(e.counters(), n_games)
         return samples_to_tuples(e.samples())
+
+
+def check_complete(c, n_games):
+    """Raise unless every requested game finished with the reference's semantics: a node
+    arena overflow skips an expansion (engine.hip k_expand), so that search is no longer the
+    reference's; dropped sample rows or unfinished games are lost data."""
+    if c["arena_overflows"]:
+        raise RuntimeError(f"node arena overflowed {c['arena_overflows']} times: the search "
+                           "diverged from the reference (raise node_capacity)")
+    if c["samples_dropped"]:
+        raise RuntimeError(f"{c['samples_dropped']} sample rows dropped: the sample buffer is "
+                           "full (raise sample_capacity)")
+    if c["games_finished"] < n_games:
+        raise RuntimeError(f"only {c['games_finished']} of {n_games} games finished within the "
+                           "step limit")

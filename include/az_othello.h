@@ -49,6 +49,9 @@ enum {
 
 const char* az_last_error(void);
 int az_abi_version(void);
+/* content hash (sha256 hex, 64 chars) of the sources and flags this library was compiled
+ * from (alphazero-othello_amd/az_build.py source_hash()): which build a process loaded */
+const char* az_build_id(void);
 
 /* ---------------- stateless board entry points: host ---------------------------- */
 
@@ -318,6 +321,15 @@ int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t channels, int32_
 int az_conv3x3_wino_gpu(const float* x, const void* wq, const float* bias, const float* res,
                         float* y, int32_t n_boards, int32_t channels, int32_t relu,
                         int32_t mode, void* stream);
+
+/* The same op, weights (az_conv3x3_wino_prep_gpu layout) and modes as az_conv3x3_wino_gpu
+ * at 128 channels (csrc/conv_wino4.hip): four boards per workgroup, the transform points
+ * visited row by row with the output transform folded after each row's K loop, so each
+ * streamed weight fragment feeds twice the boards.  Replaces the same reference layers
+ * (Models.py:72-90 ResidualBlock convs). */
+int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias, const float* res,
+                         float* y, int32_t n_boards, int32_t channels, int32_t relu,
+                         int32_t mode, void* stream);
 
 /* The whole residual trunk of AlphaZeroNet / FastOthelloNet in one launch
  * (csrc/conv_wino.hip): the stem (az_conv_stem_gpu's arithmetic) then n_blocks residual

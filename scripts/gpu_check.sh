@@ -17,7 +17,7 @@ run() {  # run <name> <timeout> cmd...
   return 0
 }
 STEPS=${STEPS:-all}
-[[ $STEPS == *pytest* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+[[ $STEPS == *pytest* || $STEPS == all ]] && run pytest_gpu 700 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench 900 python bench.py ${BENCH_ARGS:-}
 [[ $STEPS == *prof* || $STEPS == all ]] && run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --skip-cpu --steps-per-graph 1 --warmup-exact ${PROF_ARGS:---steps 400 --warmup 2000}

@@ -19,6 +19,17 @@ def declared_symbols():
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(\w+)\s*\(", src, re.M)))
 
 
+def declared_arg_counts():
+    """name -> number of parameters of every prototype in include/az_othello.h."""
+    src = open(os.path.join(ROOT, "include", "az_othello.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?\w+\*?\s+\**(\w+)\s*\(([^)]*)\)\s*;", src, re.M):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
 def test_library_exports_every_declared_symbol():
     syms = declared_symbols()
     assert len(syms) >= 25
@@ -26,6 +37,23 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(nat.lib, s), s
     assert set(nat.SIGNATURES) <= set(syms) | {"az_abi_version"}
     assert nat.lib.az_abi_version() == 1
+
+
+def test_binding_argument_counts_match_header():
+    """Every ctypes argtypes list has exactly as many entries as its C prototype (a short
+    list would pass the trailing stream as an untyped extra argument)."""
+    counts = declared_arg_counts()
+    assert len(counts) == len(declared_symbols())
+    for name, args in nat.SIGNATURES.items():
+        assert len(args) == counts[name], (name, len(args), counts[name])
+
+
+def test_loaded_library_was_built_from_this_tree():
+    """The build id embedded at compile time (sha256 of sources, headers and flags) equals
+    the hash of the tree under test: the library loaded is not a stale build."""
+    import az_build
+
+    assert nat.build_id() == az_build.source_hash() == az_build.built_id(nat.LIB_PATH)
 
 
 def own_opp(pos, neg, player):

@@ -67,7 +67,8 @@ def test_bias_act_kernel_matches_torch():
 
 
 @pytest.mark.parametrize("kind", ["az", "fast"])
-@pytest.mark.parametrize("conv,precision,algo", [("hip", "split3", "wino"), ("hip", "split3", "direct"),
+@pytest.mark.parametrize("conv,precision,algo", [("hip", "split3", "wino"), ("hip", "split3", "wino4"),
+                                                 ("hip", "split3", "direct"),
                                                  ("hip", "fp32", None), ("miopen", None, None)])
 def test_inference_copy_matches_module(kind, conv, precision, algo):
     torch.manual_seed(0)
@@ -82,7 +83,8 @@ def test_inference_copy_matches_module(kind, conv, precision, algo):
     net = net.cuda().eval()
     fused = inference_copy(net, "cuda", conv=conv, precision=precision, conv_algo=algo)
     if algo is not None:
-        assert all(c.algo == algo for c in list(fused.c1) + list(fused.c2))
+        want = "wino" if algo == "wino4" and kind == "fast" else algo  # wino4: 128 channels
+        assert all(c.algo == want for c in list(fused.c1) + list(fused.c2))
     x = torch.randint(-1, 2, (257, 64), device="cuda").float()
     with torch.no_grad():
         logits, v = net(x.view(-1, 1, 8, 8))
@@ -107,7 +109,7 @@ def _mx_conv(x, w, b, r, relu, mode):
     return y
 
 
-def _wino_conv(x, w, b, r, relu, mode):
+def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu"):
     C = x.shape[1]
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
     planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
@@ -115,10 +117,9 @@ def _wino_conv(x, w, b, r, relu, mode):
     nat.check(nat.lib.az_conv3x3_wino_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode,
                                                nat.stream_ptr()), "az_conv3x3_wino_prep_gpu")
     y = torch.empty_like(x, memory_format=torch.channels_last)
-    nat.check(nat.lib.az_conv3x3_wino_gpu(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
-                                          None if r is None else nat.ptr(r), nat.ptr(y),
-                                          x.shape[0], C, int(relu), mode, nat.stream_ptr()),
-              "az_conv3x3_wino_gpu")
+    nat.check(getattr(nat.lib, fn)(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
+                                   None if r is None else nat.ptr(r), nat.ptr(y),
+                                   x.shape[0], C, int(relu), mode, nat.stream_ptr()), fn)
     torch.cuda.synchronize()
     return y
 
@@ -182,6 +183,38 @@ def test_conv3x3_winograd_is_fp32_accurate(C, B, res, relu):
     assert e_w.max() <= 2 * e_32.max() + 1e-6, (e_w.max(), e_32.max())
     assert e_w.mean() <= 2 * e_32.mean() + 1e-8, (e_w.mean(), e_32.mean())
     torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+@pytest.mark.parametrize("B", [1, 3, 4, 5, 130, 1024])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_conv3x3_winograd4_is_fp32_accurate(B, res, relu):
+    """The four-board Winograd form (output transform folded per transform-grid row,
+    csrc/conv_wino4.hip) against fp64: the fp32-accuracy bar of the other split3 kernels,
+    board counts that leave 1-3 boards in the last workgroup included."""
+    C = 128
+    x, w, b, r, ref64 = _case(C, B, C * 19 + B)
+    rr = r if res else None
+    y = _wino_conv(x, w, b, rr, relu, nat.AZ_CONV_SPLIT3, fn="az_conv3x3_wino4_gpu")
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    y32 = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
+                                     nat.ptr(y32), B, C, int(relu), nat.stream_ptr()), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ref = ref64 + (r.cpu().double() if res else 0)
+    if relu:
+        ref = F.relu(ref)
+    e_w = (y.cpu().double() - ref).abs()
+    e_32 = (y32.cpu().double() - ref).abs()
+    assert e_w.max() <= 2 * e_32.max() + 1e-6, (e_w.max(), e_32.max())
+    assert e_w.mean() <= 2 * e_32.mean() + 1e-8, (e_w.mean(), e_32.mean())
+    torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+def test_conv3x3_winograd4_fp16_mode():
+    x, w, b, r, ref64 = _case(128, 37, 128 + 11)
+    y = _wino_conv(x, w, b, r, True, nat.AZ_CONV_FP16, fn="az_conv3x3_wino4_gpu")
+    ref = F.relu(ref64 + r.cpu().double()).float().cuda()
+    torch.testing.assert_close(y, ref, atol=5e-3, rtol=5e-3)
 
 
 @pytest.mark.parametrize("C", [64, 128])
