@@ -161,13 +161,17 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
                at 128 channels the Winograd F(2x2,3x3) form csrc/conv_wino.hip;
                tests/test_nn_gpu.py bounds both errors by the fp32 kernel's against fp64);
       "fp32":  fp32 MFMA (csrc/conv.hip);
+      "fp16x2": fp32-accurate with half of split3's products: both operands as an fp16
+               hi + lo pair after exact power-of-two scaling (per layer for the weights, per
+               board for the inputs), three products in fp32 (csrc/conv_wino4.hip, 128
+               channels; 64-channel convs fall back to split3);
       "fp16":  fp16 operands, fp32 accumulation (config #5's fp16 inference; the default
                when dtype is float16).
     Activations, the stem and the heads stay fp32 on the fused path.  conv_algo ("direct" /
     "wino") overrides default_conv_algo for the 16-bit trunk."""
     if precision is None:
         precision = "fp16" if dtype == torch.float16 else "split3"
-    assert precision in ("split3", "fp32", "fp16"), precision
+    assert precision in ("split3", "fp16x2", "fp32", "fp16"), precision
     import copy
 
     m = copy.deepcopy(net).eval()
@@ -228,6 +232,8 @@ def default_conv_algo(precision, channels):
     """The 16-bit-pipe 3x3 conv algorithm: "wino" (csrc/conv_wino.hip, Winograd F(2x2,3x3))
     where it measured faster (split3, 128 channels: profiles/r01_conv_mx.jsonl), "direct"
     (csrc/conv16.hip) elsewhere; AZ_CONV_ALGO=direct|wino overrides."""
+    if precision == "fp16x2":
+        return "wino4"
     env = os.environ.get("AZ_CONV_ALGO")
     if env in ("direct", "wino", "wino4"):
         return "wino" if env == "wino4" and channels != 128 else env
@@ -241,7 +247,7 @@ class _HipConv3x3(nn.Module):
     az_conv3x3_mx_prep_gpu) or csrc/conv_wino.hip (algo "wino": weights transformed to the
     Winograd domain and split by az_conv3x3_wino_prep_gpu)."""
 
-    MODES = {"split3": 0, "fp16": 1}  # AZ_CONV_SPLIT3, AZ_CONV_FP16
+    MODES = {"split3": 0, "fp16": 1, "fp16x2": 2}  # AZ_CONV_SPLIT3, AZ_CONV_FP16, _FP16X2
 
     def __init__(self, conv: nn.Conv2d, precision="split3", algo=None):
         super().__init__()
@@ -251,6 +257,8 @@ class _HipConv3x3(nn.Module):
         co, ci = w.shape[0], w.shape[1]
         assert co == ci and co in (64, 128) and w.shape[2:] == (3, 3)
         self.channels = co
+        if precision == "fp16x2" and co != 128:  # the scaled fp16 pair is a wino4 mode
+            precision = "split3"
         self.precision = precision
         self.algo = "direct" if precision == "fp32" else (algo or default_conv_algo(precision, co))
         if self.algo == "wino4" and co != 128:  # the 4-board form is built for 128 channels
@@ -264,13 +272,19 @@ class _HipConv3x3(nn.Module):
             planes = 3 if precision == "split3" else 1
             wino = self.algo in ("wino", "wino4")
             taps = 16 if wino else 9
-            wq = torch.empty(taps * co * ci * planes, dtype=torch.int16, device=w.device)
+            n16 = taps * co * ci * planes
+            if wino:
+                n16 = nat.lib.az_conv3x3_wino_prep_bytes(co, self.mode) // 2
+            wq = torch.empty(n16, dtype=torch.int16, device=w.device)
             prep = nat.lib.az_conv3x3_wino_prep_gpu if wino else nat.lib.az_conv3x3_mx_prep_gpu
             nat.check(prep(nat.ptr(w9), nat.ptr(wq), co, self.mode, nat.stream_ptr()),
                       "conv3x3 weight prep")
             self.wq = nn.Parameter(wq, requires_grad=False)
 
-    def forward(self, x, res=None, relu=True):
+    def forward(self, x, res=None, relu=True, in_absmax=None, out_absmax=None):
+        """in_absmax / out_absmax: float [B] per-board max |x| (consumed: reset to 0) and
+        max |y| accumulator (zeros on entry) of the wino4 kernel; fp16x2 needs in_absmax
+        (computed here when absent)."""
         import az_native as nat
 
         x = x.contiguous(memory_format=torch.channels_last)
@@ -278,14 +292,21 @@ class _HipConv3x3(nn.Module):
             res = res.contiguous(memory_format=torch.channels_last)
         y = torch.empty_like(x, memory_format=torch.channels_last)
         rp = None if res is None else nat.ptr(res)
+        if self.algo == "wino4":
+            if self.precision == "fp16x2" and in_absmax is None:
+                in_absmax = board_absmax(x)
+            nat.check(nat.lib.az_conv3x3_wino4_gpu(
+                nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp, nat.ptr(y), x.shape[0],
+                self.channels, int(relu), self.mode, nat.ptr(in_absmax), nat.ptr(out_absmax),
+                nat.stream_ptr()), "az_conv3x3_wino4_gpu")
+            return y
         if self.precision == "fp32":
             rc = nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(self.w9), nat.ptr(self.bias), rp,
                                         nat.ptr(y), x.shape[0], self.channels, int(relu),
                                         nat.stream_ptr())
             nat.check(rc, "az_conv3x3_gpu")
         else:
-            name = {"wino": "az_conv3x3_wino_gpu", "wino4": "az_conv3x3_wino4_gpu",
-                    "direct": "az_conv3x3_mx_gpu"}[self.algo]
+            name = {"wino": "az_conv3x3_wino_gpu", "direct": "az_conv3x3_mx_gpu"}[self.algo]
             rc = getattr(nat.lib, name)(nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp,
                                         nat.ptr(y), x.shape[0], self.channels, int(relu),
                                         self.mode, nat.stream_ptr())
@@ -332,6 +353,18 @@ class _HipStem(nn.Module):
                                            nat.ptr(y), x.shape[0], self.channels,
                                            nat.stream_ptr()), "az_conv_stem_gpu")
         return y
+
+
+def board_absmax(x, out=None):
+    """float [B] max |x| of each board of an NHWC [B, C, 8, 8] tensor (az_board_absmax_gpu)."""
+    import az_native as nat
+
+    x = x.contiguous(memory_format=torch.channels_last)
+    if out is None:
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    nat.check(nat.lib.az_board_absmax_gpu(nat.ptr(x), x.shape[0], x.shape[1], nat.ptr(out),
+                                          nat.stream_ptr()), "az_board_absmax_gpu")
+    return out
 
 
 def _merge_1x1(a: nn.Conv2d, b: nn.Conv2d) -> nn.Conv2d:
@@ -427,6 +460,19 @@ class FusedInferenceNet(nn.Module, Inference):
             c1s, c2s = c1s[1:], c2s[1:]
         else:
             h = self.stem(x)
+        if c1s and getattr(c1s[0], "precision", "") == "fp16x2":
+            # per-board input ranges ping-pong between two buffers: each conv consumes (and
+            # resets) one and accumulates its output's into the other
+            B = h.shape[0]
+            bufs = getattr(self, "_absmax", None)
+            if bufs is None or bufs[0].shape[0] != B or bufs[0].device != h.device:
+                bufs = self._absmax = [torch.zeros(B, dtype=torch.float32, device=h.device)
+                                       for _ in range(2)]
+            board_absmax(h, out=bufs[0])
+            for c1, c2 in zip(c1s, c2s):
+                t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1])
+                h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0])
+            return h
         for c1, c2 in zip(c1s, c2s):
             h = c2(c1(h), res=h)
         return h

@@ -67,7 +67,7 @@ _I64 = ctypes.c_int64
 _U64 = ctypes.c_uint64
 _D = ctypes.c_double
 
-AZ_CONV_SPLIT3, AZ_CONV_FP16 = 0, 1  # az_conv3x3_mx_gpu modes
+AZ_CONV_SPLIT3, AZ_CONV_FP16, AZ_CONV_FP16X2 = 0, 1, 2  # conv kernel numerics modes
 
 # name -> argtypes (restype is int for every entry point except az_last_error)
 SIGNATURES = {
@@ -112,7 +112,9 @@ SIGNATURES = {
     "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_wino_prep_gpu": [_P, _P, _I32, _I32, _P],
     "az_conv3x3_wino_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
-    "az_conv3x3_wino4_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
+    "az_conv3x3_wino4_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P],
+    "az_board_absmax_gpu": [_P, _I32, _I32, _P, _P],
+    "az_conv3x3_wino_prep_bytes": [_I32, _I32],
     "az_trunk_wino_gpu": [_P] * 7 + [_I32] * 4 + [_P],
     "az_heads_az_gpu": [_P] * 11 + [_I32, _I32, _P],
     "az_conv3x3_mx_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P],
@@ -140,6 +142,7 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _I
+    lib.az_conv3x3_wino_prep_bytes.restype = _I64
     return lib
 
 

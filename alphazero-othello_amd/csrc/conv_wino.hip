@@ -513,11 +513,22 @@ __global__ __launch_bounds__(G::THREADS) void k_trunk_wino(TrunkArgs a) {
 }
 
 // w9 [9][Co][Ci] fp32 -> U = G g G^T (fp64, rounded once to fp32) -> wq
-// [Ci/16][16 points][PLANES][Co][16] 16-bit words
-template <int MODE>
-__global__ void k_wino_prep(const float* __restrict__ w9, uint16_t* __restrict__ wq, int C) {
-  constexpr int P = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
+// [Ci/16][16 points][PLANES][Co][16] 16-bit words.  FP16X2: U * 2^su split into an fp16
+// pair; hdr = the 16-byte header after the words: [0] max |U| bits (k_wino_umax), [1] su.
+// With MAXPASS the kernel only reduces max |U| into hdr[0].
+template <int MODE, bool MAXPASS = false>
+__global__ void k_wino_prep(const float* __restrict__ w9, uint16_t* __restrict__ wq, int C,
+                            unsigned* hdr) {
+  constexpr int P = MODE == AZ_CONV_SPLIT3 ? 3 : (MODE == AZ_CONV_FP16X2 ? 2 : 1);
   const int n = C * C;
+  float usc = 1.0f;
+  if constexpr (MODE == AZ_CONV_FP16X2 && !MAXPASS) {
+    const unsigned mb = hdr[0];  // max |U| bits: max |U| < 2^e (frexp's exponent)
+    const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;
+    usc = ldexpf(1.0f, 15 - e);           // scaled max < 2^15 (fp16 max 65504)
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[1] = (unsigned)(15 - e);
+  }
+  unsigned umax = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int co = i / C, ci = i % C;
     double g[3][3];
@@ -541,7 +552,15 @@ __global__ void k_wino_prep(const float* __restrict__ w9, uint16_t* __restrict__
         const int xi = k * 4 + l;
         const size_t base = ((((size_t)(ci / 16) * 16 + xi) * P) * C + co) * 16 + (ci & 15);
         const size_t pstride = (size_t)C * 16;
-        if constexpr (MODE == AZ_CONV_SPLIT3) {
+        if constexpr (MAXPASS) {
+          umax = max(umax, __float_as_uint(fabsf(v)));
+        } else if constexpr (MODE == AZ_CONV_FP16X2) {
+          const float vs = v * usc;  // exact: a power of two
+          const _Float16 hi = (_Float16)vs;
+          const _Float16 lo = (_Float16)(vs - (float)hi);
+          wq[base] = __builtin_bit_cast(uint16_t, hi);
+          wq[base + pstride] = __builtin_bit_cast(uint16_t, lo);
+        } else if constexpr (MODE == AZ_CONV_SPLIT3) {
           const __bf16 x0 = (__bf16)v;
           const float r1 = v - (float)x0;
           const __bf16 x1 = (__bf16)r1;
@@ -554,6 +573,11 @@ __global__ void k_wino_prep(const float* __restrict__ w9, uint16_t* __restrict__
         }
       }
     }
+  }
+  if constexpr (MAXPASS) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) umax = max(umax, (unsigned)__shfl_xor((int)umax, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(hdr, umax);
   }
 }
 
@@ -635,6 +659,11 @@ extern "C" int az_trunk_wino_gpu(const float* planes, const float* stem_w, const
                         channels, mode);
 }
 
+extern "C" int64_t az_conv3x3_wino_prep_bytes(int32_t channels, int32_t mode) {
+  const int planes = mode == AZ_CONV_SPLIT3 ? 3 : (mode == AZ_CONV_FP16X2 ? 2 : 1);
+  return (int64_t)16 * channels * channels * planes * 2 + (mode == AZ_CONV_FP16X2 ? 16 : 0);
+}
+
 extern "C" int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t channels,
                                         int32_t mode, void* stream) {
   AZ_REQUIRE(w9 && wq, AZ_ERR_ARG, "az_conv3x3_wino_prep_gpu: null buffer");
@@ -644,10 +673,15 @@ extern "C" int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t chann
   const unsigned grid = (unsigned)((channels * channels + 255) / 256);
   uint16_t* out = static_cast<uint16_t*>(wq);
   if (mode == AZ_CONV_SPLIT3)
-    hipLaunchKernelGGL(k_wino_prep<AZ_CONV_SPLIT3>, dim3(grid), dim3(256), 0, s, w9, out, channels);
+    hipLaunchKernelGGL((k_wino_prep<AZ_CONV_SPLIT3>), dim3(grid), dim3(256), 0, s, w9, out, channels, nullptr);
   else if (mode == AZ_CONV_FP16)
-    hipLaunchKernelGGL(k_wino_prep<AZ_CONV_FP16>, dim3(grid), dim3(256), 0, s, w9, out, channels);
-  else
+    hipLaunchKernelGGL((k_wino_prep<AZ_CONV_FP16>), dim3(grid), dim3(256), 0, s, w9, out, channels, nullptr);
+  else if (mode == AZ_CONV_FP16X2) {
+    unsigned* hdr = reinterpret_cast<unsigned*>(out + (size_t)16 * channels * channels * 2);
+    AZ_HIP(hipMemsetAsync(hdr, 0, 16, s));
+    hipLaunchKernelGGL((k_wino_prep<AZ_CONV_FP16X2, true>), dim3(grid), dim3(256), 0, s, w9, out, channels, hdr);
+    hipLaunchKernelGGL((k_wino_prep<AZ_CONV_FP16X2>), dim3(grid), dim3(256), 0, s, w9, out, channels, hdr);
+  } else
     return azc::set_error(AZ_ERR_ARG, "az_conv3x3_wino_prep_gpu: unknown mode %d", mode);
   AZ_HIP(hipGetLastError());
   return AZ_OK;

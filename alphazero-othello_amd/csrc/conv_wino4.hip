@@ -15,28 +15,79 @@
 // folded into the four output accumulators right after its K loop:
 //     t_j(k) = sum_l A^T[j][l] M_(k,l)     (t_0 = M0 + M1 + M2, t_1 = M1 - M2 - M3)
 //     Y[i][j] += A^T[i][k] t_j(k)
-// so a wave holds 4 points' M plus the 2x2 outputs Y instead of 16 points' M: room for 64
-// tile rows (4 boards), half the weight bytes per board.
+// so a tile needs 4 points' M plus its 2x2 outputs Y live instead of 16 points' M: the
+// same registers hold 4 boards instead of 2.
 //
-// Workgroup = 4 boards (64 tiles = two 32-row MFMA tiles) x all 128 columns, 4 waves (one
-// per SIMD, 512 registers each): wave w owns columns 32w..32w+31 for all 64 rows, so each
-// weight fragment feeds two MFMA row tiles and no two waves stream the same weights.
+// Workgroup = 4 boards (64 tiles = two 32-row MFMA tiles) x all 128 columns, 8 waves (two
+// per SIMD): wave w = (row tile rt = w / 4, column block cb = w % 4).  Waves w and w + 4
+// (same columns, the other row tile) request the same weight fragments at the same step,
+// so the second request is served by the CU's L1: the L2 -> CU weight stream per board is
+// half of conv_wino.hip's.
 //   * Linear chunk L = 0..31 = (group k = L / 8, input-channel chunk c = L % 8 of 16
-//     channels); within a chunk, steps l = 0..3 run point (k, l): 2 row tiles x (6 split3
-//     products | 1 fp16 product) MFMAs.
+//     channels); within a chunk, steps l = 0..3 run point (k, l): 6 split3 products (or 1
+//     fp16 product) on the wave's 32x32 tile.
 //   * V of chunk L+1 is formed while chunk L computes: the two window rows B^T row k needs
-//     (d_a +- d_a') are loaded one chunk ahead (4 of the 16 loads per step), combined into the
-//     row at the chunk start, and each step transforms, splits and stores one point into the
-//     other half of a double-buffered LDS image [point][plane][tile][16 ch] (tile rows XOR-
-//     swizzled by 16-byte half so the ds_read_b128 fragment reads are conflict-free).
+//     (d_a +- d_a') are requested one chunk ahead, combined into the row at the chunk start,
+//     and each step transforms, splits and stores one point into the other half of a
+//     double-buffered LDS image [point][plane][tile][16 ch] (rows XOR-swizzled by 16-byte
+//     half so the ds_read_b128 fragment reads are conflict-free).
 //   * Weights stream per wave from L2 three steps ahead (ring of 4 fragments).
 //   * One LDS barrier per chunk (lgkmcnt only; the weight and window loads stay in flight).
 //   * Epilogue straight from the Y registers: + bias (+ residual), ReLU, store.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
 
+#ifndef AZ_W4_IPD3
+#define AZ_W4_IPD3 1
+#endif
+#ifndef AZ_W4_IPD16
+#define AZ_W4_IPD16 2
+#endif
+#ifndef AZ_W4_PD3
+#define AZ_W4_PD3 3
+#endif
+#ifndef AZ_W4_PD16
+#define AZ_W4_PD16 7
+#endif
+
+#ifndef AZ_W4_STAMP
+#define AZ_W4_STAMP 0
+#endif
+// experiment hooks (scripts/build_variants.py builds with bits set; results wrong):
+// 1 = no weight loads in the loop, 2 = no transform / input work in the loop, 4 = no MFMAs,
+// 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads.  Product: 0.
+#ifndef AZ_W4_EXP
+#define AZ_W4_EXP 0
+#endif
+#ifndef AZ_W4_SCHED
+#define AZ_W4_SCHED 0
+#endif
+// timing proxy of a two-plane split (wrong numerics): 2 planes, 3 products
+#ifndef AZ_W4_PROXY2
+#define AZ_W4_PROXY2 0
+#endif
+
 namespace {
+
+#if AZ_W4_STAMP
+// experiment builds only (scripts/build_variants.py -DAZ_W4_STAMP=1): per-workgroup
+// s_memtime / s_memrealtime stamps [wg][16] in a buffer no kernel reads
+__device__ unsigned long long g_w4_stamps[1024 * 16];
+#define W4_STAMP(i)                                                                  \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {                                     \
+      g_w4_stamps[blockIdx.x * 16 + 2 * (i)] = __builtin_amdgcn_s_memtime();         \
+      g_w4_stamps[blockIdx.x * 16 + 2 * (i) + 1] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                \
+  } while (0)
+#else
+#define W4_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -45,18 +96,35 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-template <int MODE_>
+template <int MODE_, int NRT_>
 struct W4 {
   static constexpr int C = 128, MODE = MODE_;
-  static constexpr int PLANES = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
-  static constexpr int BOARDS = 4, ROWS = 64, THREADS = 256;
+  static constexpr int PLANES =
+      MODE == AZ_CONV_SPLIT3 ? (AZ_W4_PROXY2 ? 2 : 3) : (MODE == AZ_CONV_FP16X2 ? 2 : 1);
+  static constexpr bool SCALED = MODE == AZ_CONV_FP16X2;  // power-of-two operand scaling
+  // NRT = MFMA row tiles per wave: 2 -> 4 waves (one per SIMD), each weight fragment feeds
+  // both row tiles of its wave; 1 -> 8 waves (two per SIMD), row-tile partners request
+  // the same fragments
+  static constexpr int NRT = NRT_, WAVES = 8 / NRT, TPT = NRT;
+  static constexpr int BOARDS = 4, ROWS = 64, THREADS = 64 * WAVES;
   static constexpr int SLAB = ROWS * 32;            // one (point, plane): 64 tiles x 16 ch x 2 B
   static constexpr int BUF = 4 * PLANES * SLAB;     // one (group, chunk): its four points
-  static constexpr int LDS_BYTES = 2 * BUF;
+  // input chunk slice staged in LDS, zero-padded to 10 x 10 positions per board so a
+  // window read never needs a mask: [board][10][10][16 ch] fp32
+  static constexpr int IN_ROW = 10 * 64, IN_BOARD = 10 * IN_ROW, IN_SLOT = BOARDS * IN_BOARD;
+  static constexpr int IN_OFF = 2 * BUF;             // two slots after the V double buffer
+  static constexpr int LDS_BYTES = 2 * BUF + 2 * IN_SLOT;
+  static constexpr int LD_PER_THREAD = BOARDS * 64 * 4 / THREADS;  // 16-byte loads per chunk
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes of one (chunk, point)
   static constexpr int CHUNKS = C / 16;
   static constexpr int LCHUNKS = 4 * CHUNKS;        // (group, chunk) pairs
   static constexpr int QSTEPS = LCHUNKS * 4;        // (group, chunk, point) steps
+  // weight fragment ring and prefetch distance (steps)
+  static constexpr int PD = MODE == AZ_CONV_FP16 ? AZ_W4_PD16 : AZ_W4_PD3;
+  static constexpr int RING = PD < 4 ? 4 : 8;  // divides the 8 steps of a chunk pair
+  // input slices requested IPD chunks ahead of their LDS store (IPD register sets)
+  static constexpr int IPD = MODE == AZ_CONV_FP16 ? AZ_W4_IPD16 : AZ_W4_IPD3;
+  static_assert(IPD == 1 || IPD == 2, "IPD");
 };
 
 template <class G>
@@ -71,9 +139,15 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// frexp's exponent of a non-negative finite float (x < 2^e; 0 -> 0), from its bits
+__device__ __forceinline__ int frexp_exp(float x) {
+  const int b = (int)((__float_as_uint(x) >> 23) & 0xff);
+  return b == 0 ? (x > 0.0f ? -125 : 0) : b - 126;
+}
+
 // window rows of group k: B^T row k = sa * d_a0 + sb * d_a1 (B^T = [1 0 -1 0; 0 1 1 0;
 // 0 -1 1 0; 0 1 0 -1]); multiplying by +-1 is exact, so this is the transform's own
-// add/subtract
+// add / subtract
 __device__ __forceinline__ int grp_a0(int k) { return k == 0 ? 0 : 1; }
 __device__ __forceinline__ int grp_a1(int k) { return k == 3 ? 3 : 2; }
 __device__ __forceinline__ float grp_sa(int k) { return k == 2 ? -1.0f : 1.0f; }
@@ -90,13 +164,13 @@ __device__ __forceinline__ void load_b(Frag<G>& f, const char* wq, int wlane, in
 }
 
 template <class G>
-__device__ __forceinline__ void read_a(Frag<G> (&a)[2], const char* buf, int l,
-                                       const int (&aoff)[2]) {
+__device__ __forceinline__ void read_a(Frag<G> (&a)[G::NRT], const char* buf, int l,
+                                       const int (&aoff)[G::NRT]) {
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int t = 0; t < G::NRT; ++t)
 #pragma unroll
     for (int pl = 0; pl < G::PLANES; ++pl)
-      a[rt].v[pl] = *reinterpret_cast<const Word8<G>*>(buf + (l * G::PLANES + pl) * G::SLAB + aoff[rt]);
+      a[t].v[pl] = *reinterpret_cast<const Word8<G>*>(buf + (l * G::PLANES + pl) * G::SLAB + aoff[t]);
 }
 
 template <class G>
@@ -104,45 +178,68 @@ __device__ __forceinline__ void mma(f32x16& acc, const Frag<G>& a, const Frag<G>
   if constexpr (G::MODE == AZ_CONV_SPLIT3) {
     // smallest partial products first (x2y0, x1y1, x0y2, x1y0, x0y1, x0y0)
     constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+    constexpr int T0 = AZ_W4_PROXY2 ? 3 : 0;  // proxy: the last three products only
 #pragma unroll
-    for (int t = 0; t < 6; ++t)
+    for (int t = T0; t < 6; ++t)
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[PA[t]], b.v[PB[t]], acc, 0, 0, 0);
+  } else if constexpr (G::MODE == AZ_CONV_FP16X2) {
+    // lo * hi, hi * lo, hi * hi (the lo * lo term is below fp32's rounding unit)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[1], b.v[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[0], acc, 0, 0, 0);
   } else {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[0], acc, 0, 0, 0);
   }
 }
 
-// window entries e0..e0+NE-1 (e = which * 4 + b: window row a0 / a1 of linear chunk L's
-// group, column b) of transform item u.  Off-board entries read element 0 (a valid
-// address) and are zeroed in make_rows, so every load is issued unconditionally.
-template <class G, int NE>
-__device__ __forceinline__ void load_raw(f32x2 (&raw)[2][8], const float* x, const int (&off)[2],
-                                         const int (&msk)[2], int L, int u, int e0) {
-  const int k = L >> 3, c = L & 7;
-  const int a0 = grp_a0(k), a1 = grp_a1(k);
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// the chunk-L slice of the workgroup's input (4 boards x 64 positions x 16 channels fp32):
+// LD_PER_THREAD coalesced 16-byte loads per thread into registers ...
+template <class G>
+__device__ __forceinline__ void load_in(f32x4 (&ld)[G::LD_PER_THREAD], const float* x,
+                                        const int (&goff)[G::LD_PER_THREAD], int L) {
+  const int c = L & 7;
 #pragma unroll
-  for (int i = 0; i < NE; ++i) {
-    const int e = e0 + i, b = e & 3, a = (e >> 2) ? a1 : a0;
-    const bool in = (msk[u] >> (a * 4 + b)) & 1;
-    const uint32_t o = in ? (uint32_t)(off[u] + (a * 8 + b) * G::C + c * 16) : 0u;
-    raw[u][e] = *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(x) + o * 4u);
+  for (int j = 0; j < G::LD_PER_THREAD; ++j)
+    ld[j] = *reinterpret_cast<const f32x4*>(x + goff[j] + c * 16);
+}
+
+// ... and into the slot's padded interior
+template <class G>
+__device__ __forceinline__ void store_in(char* slot, const f32x4 (&ld)[G::LD_PER_THREAD],
+                                         const int (&ldst)[G::LD_PER_THREAD]) {
+#pragma unroll
+  for (int j = 0; j < G::LD_PER_THREAD; ++j) *reinterpret_cast<f32x4*>(slot + ldst[j]) = ld[j];
+}
+
+// B^T row k of this item's 4x4 window (channel pair): the two window rows a0, a1 of group
+// k read from the padded slot (off-board entries are the zero border) -- issued first,
+// combined once the MFMAs they hide behind are under way
+template <class G>
+__device__ __forceinline__ void read_rows(f32x2 (&d)[8], const char* slot, int rbase, int L) {
+  const int k = L >> 3;
+  const char* r0 = slot + rbase + grp_a0(k) * G::IN_ROW;
+  const char* r1 = slot + rbase + grp_a1(k) * G::IN_ROW;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    d[b] = *reinterpret_cast<const f32x2*>(r0 + b * 64);
+    d[4 + b] = *reinterpret_cast<const f32x2*>(r1 + b * 64);
   }
 }
 
-template <class G>
-__device__ __forceinline__ void make_rows(f32x2 (&rk)[2][4], const f32x2 (&raw)[2][8],
-                                          const int (&msk)[2], int L) {
+__device__ __forceinline__ void combine_rows(f32x2 (&rk)[4], const f32x2 (&d)[8], int L) {
   const int k = L >> 3;
-  const int a0 = grp_a0(k), a1 = grp_a1(k);
   const f32x2 sa = {grp_sa(k), grp_sa(k)}, sb = {grp_sb(k), grp_sb(k)};
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const f32x2 d0 = (msk[u] >> (a0 * 4 + b)) & 1 ? raw[u][b] : f32x2{0.0f, 0.0f};
-      const f32x2 d1 = (msk[u] >> (a1 * 4 + b)) & 1 ? raw[u][4 + b] : f32x2{0.0f, 0.0f};
-      rk[u][b] = sa * d0 + sb * d1;
-    }
+  for (int b = 0; b < 4; ++b) rk[b] = sa * d[b] + sb * d[4 + b];
+}
+
+template <class G>
+__device__ __forceinline__ void make_rows(f32x2 (&rk)[4], const char* slot, int rbase, int L) {
+  f32x2 d[8];
+  read_rows<G>(d, slot, rbase, L);
+  combine_rows(rk, d, L);
 }
 
 // V at point (k, l) = (row k of B^T d) B: column combination l
@@ -156,216 +253,379 @@ __device__ __forceinline__ f32x2 col_comb(const f32x2 (&rk)[4]) {
 
 // split two transformed values into PLANES 16-bit words and store them in their slabs
 template <class G>
-__device__ __forceinline__ void put(char* slab, f32x2 v) {
-  if constexpr (G::MODE == AZ_CONV_SPLIT3) {
+__device__ __forceinline__ void put(char* slab, f32x2 v, float vsc) {
+  if constexpr (G::MODE == AZ_CONV_FP16X2) {
+    const f32x2 vs = v * vsc;  // exact: a power of two
+    const f16x2 hi = __builtin_convertvector(vs, f16x2);
+    const f16x2 lo = __builtin_convertvector(vs - __builtin_convertvector(hi, f32x2), f16x2);
+    *reinterpret_cast<f16x2*>(slab) = hi;
+    *reinterpret_cast<f16x2*>(slab + G::SLAB) = lo;
+  } else if constexpr (G::MODE == AZ_CONV_SPLIT3) {
     const bf16x2 x0 = __builtin_convertvector(v, bf16x2);
     const f32x2 r1 = v - __builtin_convertvector(x0, f32x2);
     const bf16x2 x1 = __builtin_convertvector(r1, bf16x2);
     const bf16x2 x2 = __builtin_convertvector(r1 - __builtin_convertvector(x1, f32x2), bf16x2);
     *reinterpret_cast<bf16x2*>(slab) = x0;
     *reinterpret_cast<bf16x2*>(slab + G::SLAB) = x1;
-    *reinterpret_cast<bf16x2*>(slab + 2 * G::SLAB) = x2;
+    if (G::PLANES > 2) *reinterpret_cast<bf16x2*>(slab + 2 * G::SLAB) = x2;
   } else {
     *reinterpret_cast<f16x2*>(slab) = __builtin_convertvector(v, f16x2);
   }
 }
 
 template <class G, int l>
-__device__ __forceinline__ void put_point(char* buf, const f32x2 (&rk)[2][4], const int (&soff)[2]) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) put<G>(buf + l * G::PLANES * G::SLAB + soff[u], col_comb<l>(rk[u]));
+__device__ __forceinline__ void put_point(char* buf, const f32x2 (&rk)[4], int soff, float vsc) {
+  put<G>(buf + l * G::PLANES * G::SLAB + soff, col_comb<l>(rk), vsc);
 }
 
-// group k's M (acc[l][rt]) into the output accumulators Y[i][j][rt]
-__device__ __forceinline__ void fold(f32x16 (&acc)[4][2], f32x16 (&Y)[2][2][2], int k) {
+// group K's M (acc[l][t]) into the output accumulators Y[i][j][t]; K is a compile-time
+// constant so every update is straight-line register arithmetic
+template <class G, int K>
+__device__ __forceinline__ void fold(f32x16 (&acc)[4][G::NRT], f32x16 (&Y)[2][2][G::NRT]) {
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int t = 0; t < G::NRT; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const float m0 = acc[0][rt][e], m1 = acc[1][rt][e], m2 = acc[2][rt][e], m3 = acc[3][rt][e];
+      const float m0 = acc[0][t][e], m1 = acc[1][t][e], m2 = acc[2][t][e], m3 = acc[3][t][e];
       const float t0 = (m0 + m1) + m2, t1 = (m1 - m2) - m3;
-      if (k == 0) {
-        Y[0][0][rt][e] = t0;
-        Y[0][1][rt][e] = t1;
-      } else if (k == 1) {
-        Y[0][0][rt][e] += t0;
-        Y[0][1][rt][e] += t1;
-        Y[1][0][rt][e] = t0;
-        Y[1][1][rt][e] = t1;
-      } else if (k == 2) {
-        Y[0][0][rt][e] += t0;
-        Y[0][1][rt][e] += t1;
-        Y[1][0][rt][e] -= t0;
-        Y[1][1][rt][e] -= t1;
+      if constexpr (K == 0) {
+        Y[0][0][t][e] = t0;
+        Y[0][1][t][e] = t1;
+      } else if constexpr (K == 1) {
+        Y[0][0][t][e] += t0;
+        Y[0][1][t][e] += t1;
+        Y[1][0][t][e] = t0;
+        Y[1][1][t][e] = t1;
+      } else if constexpr (K == 2) {
+        Y[0][0][t][e] += t0;
+        Y[0][1][t][e] += t1;
+        Y[1][0][t][e] -= t0;
+        Y[1][1][t][e] -= t1;
       } else {
-        Y[1][0][rt][e] -= t0;
-        Y[1][1][rt][e] -= t1;
+        Y[1][0][t][e] -= t0;
+        Y[1][1][t][e] -= t1;
       }
+    }
+  // materialise Y here: otherwise the compiler sinks the fold arithmetic past the next
+  // group's K loop, keeping this group's M live beside the next one's (and spills)
+#pragma unroll
+  for (int t = 0; t < G::NRT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if constexpr (K <= 2) asm volatile("" : "+v"(Y[0][0][t][e]), "+v"(Y[0][1][t][e]));
+      if constexpr (K >= 1) asm volatile("" : "+v"(Y[1][0][t][e]), "+v"(Y[1][1][t][e]));
     }
 }
 
-template <class G, bool RES, bool RELU>
-__global__ __launch_bounds__(256, 1) void k_conv3x3_wino4(const float* __restrict__ x,
-                                                          const char* __restrict__ wq,
-                                                          const float* __restrict__ bias,
-                                                          const float* __restrict__ res,
-                                                          float* __restrict__ y, int n_boards) {
-  constexpr int C = G::C;
-  extern __shared__ float4 lds4[];
-  char* lds = reinterpret_cast<char*>(lds4);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int col0 = 32 * wave;
-  const int b0 = blockIdx.x * G::BOARDS;
-  const int nb = n_boards - b0 < G::BOARDS ? n_boards - b0 : G::BOARDS;
-  const int wlane = (col0 + r) * 32 + h * 16;
-  const int aoff[2] = {r * 32 + ((h ^ ((r >> 3) & 1)) << 4),
-                       (32 + r) * 32 + ((h ^ ((r >> 3) & 1)) << 4)};
+// a wave's loop state (registers after inlining; one struct so the chunk and group bodies
+// below can be separate force-inlined functions)
+template <class G>
+struct St {
+  f32x4 ld[G::IPD][G::LD_PER_THREAD];
+  f32x2 rk[G::TPT][4], dr[G::TPT][8];
+  Frag<G> bf[G::RING], af[G::NRT];
+  f32x16 acc[4][G::NRT];
+  f32x16 Y[2][2][G::NRT];
+  int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], soff[G::TPT], aoff[G::NRT];
+  float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
+  int wlane;
+  const float* x;
+  const char* wq;
+  char* lds;
+};
 
-  // transform items: u = 0, 1 -> tile T = tid / 8 + 32u (board T / 16, tile row (T / 4) % 4,
-  // tile column T % 4), channel pair p = tid % 8 of each 16-channel chunk
-  int off[2], msk[2], soff[2];
+// one chunk L (of parity PAR, so a step's weight ring slot is a compile-time constant): its
+// four steps, the next chunk's transform into the other LDS buffer, the windows of the
+// chunk after that requested
+template <class G, int PAR>
+__device__ __forceinline__ void run_chunk(St<G>& S, int L) {
+  const char* cur = S.lds + (L & 1) * G::BUF;
+  char* nxt = S.lds + ((L + 1) & 1) * G::BUF;
+  // chunk L+1's rows (its windows were requested during chunk L-1); the last chunk
+  // transforms a clamped duplicate into the idle buffer (uniform body)
+  const int Lr = L + 1 < G::LCHUNKS ? L + 1 : G::LCHUNKS - 1;
+  const int Ll = L + 1 + G::IPD < G::LCHUNKS ? L + 1 + G::IPD : G::LCHUNKS - 1;  // loaded
+  const int Ls = L + 2 < G::LCHUNKS ? L + 2 : G::LCHUNKS - 1;                    // stored
+  constexpr int set_l = G::IPD == 1 ? 0 : (PAR + 1) & 1, set_s = G::IPD == 1 ? 0 : PAR;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int T = (tid >> 3) + 32 * u, p = tid & 7;
-    const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-    int m = 0;
+  for (int l = 0; l < 4; ++l) {
+    Frag<G> an[G::NRT];
+    if (l < 3 && !(AZ_W4_EXP & 16)) read_a<G>(an, cur, l + 1, S.aoff);
+    if (l < 3 && (AZ_W4_EXP & 16)) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int t = 0; t < G::NRT; ++t) an[t] = S.af[t];
+    }
+    const int slot = (4 * PAR + l) % G::RING;  // = step % RING (folds: l is unrolled)
+    if (!(AZ_W4_EXP & 4)) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int yy = 2 * ty - 1 + a, xx = 2 * tx - 1 + b;
-        m |= (bd < nb && (unsigned)yy < 8u && (unsigned)xx < 8u) << (a * 4 + b);
-      }
-    msk[u] = m;
-    off[u] = ((b0 + bd) * 64 + (2 * ty - 1) * 8 + (2 * tx - 1)) * C + 2 * p;
-    soff[u] = T * 32 + (((p >> 2) ^ ((T >> 3) & 1)) << 4) + (p & 3) * 4;
-  }
-
-  f32x2 raw[2][8], rk[2][4];
-  Frag<G> bf[4];
-  // ---- prologue: chunk 0's windows, chunk 1's windows and the first three weight steps in
-  // flight together; chunk 0 transformed into buffer 0
-  {
-    f32x2 raw0[2][8];
+      for (int t = 0; t < G::NRT; ++t) mma<G>(S.acc[l][t], S.af[t], S.bf[slot]);
+    }
+    if (l == 0 && !(AZ_W4_EXP & 2)) {
+      // chunk L+1's window rows (requested right after the previous barrier) combined
+      // behind step 0's MFMAs
 #pragma unroll
-    for (int u = 0; u < 2; ++u) load_raw<G, 8>(raw0, x, off, msk, 0, u, 0);
+      for (int u = 0; u < G::TPT; ++u) combine_rows(S.rk[u], S.dr[u], Lr);
+    }
+    const int q = L * 4 + l + G::PD;
+    if (!(AZ_W4_EXP & 1))
+      load_b<G>(S.bf[(slot + G::PD) % G::RING], S.wq, S.wlane, q < G::QSTEPS - 1 ? q : G::QSTEPS - 1);
+    // the chunk-after-next's input slice at the chunk's first step: four steps of latency
+    // cover before it is stored to LDS at the chunk's end
+    if (l == 0 && !(AZ_W4_EXP & 2)) load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) load_raw<G, 8>(raw, x, off, msk, 1, u, 0);
+    for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
+      if (l == 0) put_point<G, 0>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
+      if (l == 1) put_point<G, 1>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
+      if (l == 2) put_point<G, 2>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
+      if (l == 3) put_point<G, 3>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
+    }
+    if (l < 3) {
+#pragma unroll
+      for (int t = 0; t < G::NRT; ++t) S.af[t] = an[t];
+    }
+#if AZ_W4_SCHED
+    // interleave: each MFMA followed by a share of the step's VALU and one LDS access, the
+    // global loads behind (compile-time instruction placement; the step ends at a barrier)
+#pragma unroll
+    for (int i = 0; i < 2 * G::NRT * (G::MODE == AZ_CONV_SPLIT3 ? 6 : 1); ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, AZ_W4_SCHED, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    }
+    __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);  // VMEM read
+#endif
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) load_b<G>(bf[i], wq, wlane, i);
-    __builtin_amdgcn_sched_barrier(0);
-    make_rows<G>(rk, raw0, msk, 0);
   }
-  put_point<G, 0>(lds, rk, soff);
-  put_point<G, 1>(lds, rk, soff);
-  put_point<G, 2>(lds, rk, soff);
-  put_point<G, 3>(lds, rk, soff);
-  lds_barrier();
+  // slot (L+2) & 1 = L & 1 held chunk L's input, whose rows were formed in chunk L-1
+  if (!(AZ_W4_EXP & 2)) store_in<G>(S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
+  if (!(AZ_W4_EXP & 8)) lds_barrier();
+  read_a<G>(S.af, nxt, 0, S.aoff);
+  // the next chunk's window rows (chunk L+2, stored just before the barrier)
+#pragma unroll
+  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u)
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.rbase[u], Ls);
+}
 
-  f32x16 acc[4][2];
+template <class G>
+__device__ __forceinline__ void zero_acc(St<G>& S) {
 #pragma unroll
   for (int l = 0; l < 4; ++l)
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int t = 0; t < G::NRT; ++t)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[l][rt][e] = 0.0f;
-  f32x16 Y[2][2][2];
+      for (int e = 0; e < 16; ++e) S.acc[l][t][e] = 0.0f;
+}
 
-  Frag<G> af[2];
-  read_a<G>(af, lds, 0, aoff);
-  for (int L = 0; L < G::LCHUNKS; ++L) {
-    const char* cur = lds + (L & 1) * G::BUF;
-    char* nxt = lds + ((L + 1) & 1) * G::BUF;
-    // chunk L+1's rows (its windows were requested during chunk L-1); the last chunk
-    // transforms a clamped duplicate into the idle buffer (uniform body)
-    const int Lr = L + 1 < G::LCHUNKS ? L + 1 : G::LCHUNKS - 1;
-    const int Ll = L + 2 < G::LCHUNKS ? L + 2 : G::LCHUNKS - 1;
-    make_rows<G>(rk, raw, msk, Lr);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      Frag<G> an[2];
-      if (l < 3) read_a<G>(an, cur, l + 1, aoff);
-      mma<G>(acc[l][0], af[0], bf[l]);
-      mma<G>(acc[l][1], af[1], bf[l]);
-      const int q = L * 4 + l + 3;
-      load_b<G>(bf[(l + 3) & 3], wq, wlane, q < G::QSTEPS - 1 ? q : G::QSTEPS - 1);
-      load_raw<G, 4>(raw, x, off, msk, Ll, l >> 1, 4 * (l & 1));
-      if (l == 0) put_point<G, 0>(nxt, rk, soff);
-      if (l == 1) put_point<G, 1>(nxt, rk, soff);
-      if (l == 2) put_point<G, 2>(nxt, rk, soff);
-      if (l == 3) put_point<G, 3>(nxt, rk, soff);
-      if (l < 3) {
-        af[0] = an[0];
-        af[1] = an[1];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if ((L & 7) == 7) {
-      fold(acc, Y, L >> 3);
-#pragma unroll
-      for (int l = 0; l < 4; ++l)
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[l][rt][e] = 0.0f;
-    }
-    lds_barrier();
-    read_a<G>(af, nxt, 0, aoff);
+// transform-grid row K (compile time): its eight chunks, then the fold
+template <class G, int K>
+__device__ __forceinline__ void run_group(St<G>& S) {
+#pragma unroll 1
+  for (int c = 0; c < G::CHUNKS; c += 2) {
+    run_chunk<G, 0>(S, K * G::CHUNKS + c);
+    run_chunk<G, 1>(S, K * G::CHUNKS + c + 1);
   }
+  fold<G, K>(S.acc, S.Y);
+  zero_acc<G>(S);
+}
+
+template <class G, bool RES, bool RELU>
+__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
+    const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
+    const float* __restrict__ res, float* __restrict__ y, int n_boards,
+    float* __restrict__ in_absmax, float* __restrict__ out_absmax) {
+  constexpr int C = G::C;
+  extern __shared__ float4 lds4[];
+  W4_STAMP(0);
+  St<G> S;
+  S.lds = reinterpret_cast<char*>(lds4);
+  S.x = x;
+  S.wq = wq;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = wave & 3, rt0 = G::NRT == 1 ? wave >> 2 : 0;
+  const int r = lane & 31, h = lane >> 5;
+  const int col0 = 32 * cb;
+  const int b0 = blockIdx.x * G::BOARDS;
+  const int nb = n_boards - b0 < G::BOARDS ? n_boards - b0 : G::BOARDS;
+  S.wlane = (col0 + r) * 32 + h * 16;
+#pragma unroll
+  for (int t = 0; t < G::NRT; ++t)
+    S.aoff[t] = (32 * (rt0 + t) + r) * 32 + ((h ^ ((r >> 3) & 1)) << 4);
+
+  // transform items u: tile T = tid / 8 + u * THREADS / 8 (board T / 16, tile row
+  // (T / 4) % 4, tile column T % 4), channel pair p = tid % 8 of each 16-channel chunk;
+  // the window's top-left entry in the padded slot is position (2ty, 2tx)
+#pragma unroll
+  for (int u = 0; u < G::TPT; ++u) {
+    const int T = (tid >> 3) + u * (G::THREADS / 8), p = tid & 7;
+    const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
+    S.rbase[u] = bd * G::IN_BOARD + 2 * ty * G::IN_ROW + 2 * tx * 64 + p * 8;
+    S.soff[u] = T * 32 + (((p >> 2) ^ ((T >> 3) & 1)) << 4) + (p & 3) * 4;
+    S.vsc[u] = 1.0f;
+    if constexpr (G::SCALED) {
+      // |V| <= 4 max |x| < 2^(e+2): scaled by 2^(13-e), the transformed inputs stay below
+      // 2^15 (fp16's largest power of two)
+      const int e = frexp_exp(bd < nb ? in_absmax[b0 + bd] : 0.0f);
+      S.vsc[u] = ldexpf(1.0f, 13 - e);
+    }
+  }
+  // input loads: element e = j * THREADS + tid -> position P = e / 4 (board P / 64, clamped
+  // to the last valid board: rows of absent boards are computed but never stored),
+  // channel quad e % 4 of the chunk
+#pragma unroll
+  for (int j = 0; j < G::LD_PER_THREAD; ++j) {
+    const int e = j * G::THREADS + tid, P = e >> 2, q = e & 3;
+    const int bd = P >> 6, pos = P & 63;
+    const int bs = bd < nb ? bd : nb - 1;
+    S.goff[j] = ((b0 + bs) * 64 + pos) * C + 4 * q;
+    S.ldst[j] = bd * G::IN_BOARD + ((pos >> 3) + 1) * G::IN_ROW + ((pos & 7) + 1) * 64 + q * 16;
+  }
+
+  // ---- prologue: zero both input slots (their borders stay zero), chunk 0 and 1 slices and
+  // the first weight steps in flight together; chunk 0 transformed into V buffer 0
+  {
+    char* in0 = S.lds + G::IN_OFF;
+    for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
+      *reinterpret_cast<f32x4*>(in0 + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 ld0[G::LD_PER_THREAD], ld1[G::LD_PER_THREAD];
+    load_in<G>(ld0, x, S.goff, 0);
+    load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, x, S.goff, 1);
+    if (G::IPD == 2) load_in<G>(S.ld[0], x, S.goff, 2);  // stored at the end of chunk 0
+#pragma unroll
+    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, i);
+    lds_barrier();  // the zero fill before any interior store
+    store_in<G>(in0, ld0, S.ldst);
+    store_in<G>(in0 + G::IN_SLOT, G::IPD == 1 ? S.ld[0] : ld1, S.ldst);
+    if (G::IPD == 1) load_in<G>(S.ld[0], x, S.goff, 2);  // stored at the end of chunk 0
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], 0);
+  }
+#pragma unroll
+  for (int u = 0; u < G::TPT; ++u) {
+    put_point<G, 0>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
+    put_point<G, 1>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
+    put_point<G, 2>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
+    put_point<G, 3>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
+  }
+  lds_barrier();
+
+  zero_acc<G>(S);
+  read_a<G>(S.af, S.lds, 0, S.aoff);
+#pragma unroll
+  for (int u = 0; u < G::TPT; ++u)
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], 1);
+  W4_STAMP(1);
+  run_group<G, 0>(S);
+  W4_STAMP(2);
+  run_group<G, 1>(S);
+  W4_STAMP(3);
+  run_group<G, 2>(S);
+  W4_STAMP(4);
+  run_group<G, 3>(S);
+  W4_STAMP(5);
 
   // ---- epilogue: accumulator element e of row tile rt = tile 32rt + (e&3) + 8(e>>2) + 4h,
   // column col0 + r; Y[i][j] = output (2ty + i, 2tx + j)
   const int co = col0 + r;
   const float bv = bias[co];
+  // FP16X2: M carries 2^(su + sv_board); removing it is an exact power-of-two product
+  float unsc[2 * G::NRT];  // per board of this wave's row tiles: tile 32t + ... -> 2t + (e >= 8)
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int i = 0; i < 2 * G::NRT; ++i) unsc[i] = 1.0f;
+  if constexpr (G::SCALED) {
+    const int su = reinterpret_cast<const int*>(wq + (size_t)G::QSTEPS * G::STEP_BYTES)[1];
+#pragma unroll
+    for (int i = 0; i < 2 * G::NRT; ++i) {
+      const int bd = 2 * rt0 + i;
+      const int e = frexp_exp(bd < nb ? in_absmax[b0 + bd] : 0.0f);
+      unsc[i] = ldexpf(1.0f, -(su + 13 - e));
+    }
+  }
+  float bmax[2 * G::NRT];
+#pragma unroll
+  for (int i = 0; i < 2 * G::NRT; ++i) bmax[i] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < G::NRT; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int T = 32 * rt + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int T = 32 * (rt0 + t) + (e & 3) + 8 * (e >> 2) + 4 * h;
       const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-      if (bd >= nb) continue;  // uniform over the wave half
+      if (bd >= nb) continue;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const size_t o = ((size_t)(b0 + bd) * 64 + (2 * ty + i) * 8 + 2 * tx + j) * C + co;
-          float v = Y[i][j][rt][e] + bv;
+          float v = (G::SCALED ? S.Y[i][j][t][e] * unsc[2 * t + (e >> 3)] : S.Y[i][j][t][e]) + bv;
           if (RES) v += res[o];
           if (RELU) v = fmaxf(v, 0.0f);
           y[o] = v;
+          bmax[2 * t + (e >> 3)] = fmaxf(bmax[2 * t + (e >> 3)], fabsf(v));
         }
     }
+  if (out_absmax) {  // the next layer's in_absmax: one atomic per (wave, board)
+#pragma unroll
+    for (int i = 0; i < 2 * G::NRT; ++i) {
+      float m = bmax[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+      const int bd = 2 * rt0 + i;
+      if (lane == 0 && bd < nb)
+        atomicMax(reinterpret_cast<unsigned*>(out_absmax) + b0 + bd, __float_as_uint(m));
+    }
+  }
+  // in_absmax is consumed: reset for its next use as some layer's out_absmax (every thread
+  // read its entries in the prologue, before the first barrier)
+  if (G::SCALED && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
+  W4_STAMP(6);
 }
 
 template <class G>
 int launch_wino4(const float* x, const void* wq, const float* bias, const float* res, float* y,
-                 int n_boards, int relu, hipStream_t s) {
+                 int n_boards, int relu, float* in_absmax, float* out_absmax, hipStream_t s) {
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in once per kernel
+  if (!attr_set) {
+    const void* ks[] = {(const void*)k_conv3x3_wino4<G, true, true>,
+                        (const void*)k_conv3x3_wino4<G, true, false>,
+                        (const void*)k_conv3x3_wino4<G, false, true>,
+                        (const void*)k_conv3x3_wino4<G, false, false>};
+    for (const void* k : ks)
+      AZ_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)G::LDS_BYTES));
+    attr_set = true;
+  }
   const char* w = static_cast<const char*>(wq);
   const dim3 blk(G::THREADS);
   const size_t lds = G::LDS_BYTES;
   if (res && relu)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
   else if (res)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
   else if (relu)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
   else
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
 
 }  // namespace
 
+#if AZ_W4_STAMP
+extern "C" int az_w4_stamps(unsigned long long* host, int n) {
+  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_stamps), sizeof(unsigned long long) * n));
+  return AZ_OK;
+}
+#endif
+
 extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias,
                                     const float* res, float* y, int32_t n_boards,
-                                    int32_t channels, int32_t relu, int32_t mode, void* stream) {
+                                    int32_t channels, int32_t relu, int32_t mode,
+                                    float* in_absmax, float* out_absmax, void* stream) {
   AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_gpu: n_boards < 0");
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(x && wq && bias && y && x != y && (!res || res != y), AZ_ERR_ARG,
@@ -374,10 +634,46 @@ extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float*
              "az_conv3x3_wino4_gpu: buffers must be 16-byte aligned");
   AZ_REQUIRE(channels == 128, AZ_ERR_ARG, "az_conv3x3_wino4_gpu: channels must be 128, got %d",
              channels);
+  AZ_REQUIRE(mode != AZ_CONV_FP16X2 || (in_absmax && in_absmax != out_absmax), AZ_ERR_ARG,
+             "az_conv3x3_wino4_gpu: FP16X2 needs in_absmax (distinct from out_absmax)");
   hipStream_t s = azc::as_stream(stream);
-  if (mode == AZ_CONV_SPLIT3)
-    return launch_wino4<W4<AZ_CONV_SPLIT3>>(x, wq, bias, res, y, n_boards, relu, s);
-  if (mode == AZ_CONV_FP16)
-    return launch_wino4<W4<AZ_CONV_FP16>>(x, wq, bias, res, y, n_boards, relu, s);
+  // AZ_W4_NRT (experiments): 1 = eight waves of one row tile, 2 = four waves of two
+  static const int nrt = getenv("AZ_W4_NRT") ? atoi(getenv("AZ_W4_NRT")) : 2;
+#define W4_GO(M, N) launch_wino4<W4<M, N>>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, s)
+  if (mode == AZ_CONV_SPLIT3) return nrt == 1 ? W4_GO(AZ_CONV_SPLIT3, 1) : W4_GO(AZ_CONV_SPLIT3, 2);
+  if (mode == AZ_CONV_FP16) return nrt == 1 ? W4_GO(AZ_CONV_FP16, 1) : W4_GO(AZ_CONV_FP16, 2);
+  if (mode == AZ_CONV_FP16X2) return nrt == 1 ? W4_GO(AZ_CONV_FP16X2, 1) : W4_GO(AZ_CONV_FP16X2, 2);
+#undef W4_GO
   return azc::set_error(AZ_ERR_ARG, "az_conv3x3_wino4_gpu: unknown mode %d", mode);
+}
+
+namespace {
+// one workgroup per board: max |x| over its 64 * C values
+__global__ void k_board_absmax(const float* __restrict__ x, int per_board, float* __restrict__ out) {
+  const float4* p = reinterpret_cast<const float4*>(x + (size_t)blockIdx.x * per_board);
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < per_board / 4; i += blockDim.x) {
+    const float4 v = p[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  __shared__ float s_m[4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+}
+}  // namespace
+
+extern "C" int az_board_absmax_gpu(const float* x, int32_t n_boards, int32_t channels, float* out,
+                                   void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && channels > 0 && channels % 4 == 0, AZ_ERR_ARG,
+             "az_board_absmax_gpu: bad sizes");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(x && out && (uintptr_t)x % 16 == 0, AZ_ERR_ARG,
+             "az_board_absmax_gpu: null or unaligned buffer");
+  hipLaunchKernelGGL(k_board_absmax, dim3(n_boards), dim3(256), 0, azc::as_stream(stream), x,
+                     64 * channels, out);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
 }

@@ -66,6 +66,8 @@ L2_PEAK_TBPS = 34.5        # aggregate L2 bandwidth, 8 XCDs x 4 MiB (MI355X_MICR
 DTYPE_LABEL = {
     "split3": "fp32-accurate net (trunk: fp32 operands split into 3 bf16 words, 6 bf16 MFMA "
               "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
+    "fp16x2": "fp32-accurate net (trunk: fp32 operands as scaled fp16 hi+lo pairs, 3 fp16 MFMA "
+              "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
     "fp32": "fp32 (net), int64 bitboards",
     "fp16": "fp16 trunk operands, fp32 accumulation (net), int64 bitboards",
 }
@@ -91,10 +93,12 @@ def parse():
     ap.add_argument("--games", type=int, default=None, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--net", default=None, choices=["az5x128", "fast"])
-    ap.add_argument("--conv-precision", default=None, choices=["split3", "fp32", "fp16"],
-                    help="3x3 trunk arithmetic: split3 = bf16x3-split operands on the 16-bit "
-                         "MFMA pipe, fp32 accumulation, fp32-accurate (default for c2/c3); "
-                         "fp32 = fp32 MFMA; fp16 = fp16 operands (c5's fp16 inference)")
+    ap.add_argument("--conv-precision", default=None, choices=["fp16x2", "split3", "fp32", "fp16"],
+                    help="3x3 trunk arithmetic: fp16x2 = scaled fp16 hi+lo operand pairs, 3 "
+                         "products, fp32 accumulation, fp32-accurate (default for c2-c4; "
+                         "64-channel convs use split3); split3 = bf16x3-split operands, 6 "
+                         "products, fp32-accurate; fp32 = fp32 MFMA; fp16 = fp16 operands "
+                         "(c5's fp16 inference)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="simulation steps captured per HIP graph (1 under rocprofv3: its "
@@ -114,7 +118,7 @@ def parse():
     a.sims = a.sims or preset[1]
     a.net = a.net or preset[2]
     a.d4, a.precision = preset[3], preset[4]
-    a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "split3")
+    a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "fp16x2")
     return a
 
 
@@ -219,6 +223,7 @@ def conv_roofline(sp, device, n_boards):
 
     conv = sp.net.c2[0]
     C = conv.channels
+    refill = lambda: None  # noqa: E731  (wino4: restore the consumed per-board ranges)
     # post-ReLU-like synthetic activations (about half zeros, as the trunk's inputs are):
     # MFMA power -- and with it the clock the chip holds -- depends on the operand values
     x = torch.randn(n_boards, C, 8, 8, device=device).relu().contiguous(
@@ -231,28 +236,54 @@ def conv_roofline(sp, device, n_boards):
                 n_boards, C, 1, nat.stream_ptr()]
         kname, mult, peak = "k_conv3x3 (az_conv3x3_gpu, fp32 MFMA)", 1, MFMA32_PEAK
     else:
-        wino = getattr(conv, "algo", "direct") == "wino"
-        fn = nat.lib.az_conv3x3_wino_gpu if wino else nat.lib.az_conv3x3_mx_gpu
+        algo = getattr(conv, "algo", "direct")
         args = [nat.ptr(x), nat.ptr(conv.wq), nat.ptr(conv.bias), nat.ptr(r), nat.ptr(y),
-                n_boards, C, 1, conv.mode, nat.stream_ptr()]
-        mult = 6 if conv.precision == "split3" else 1
-        if wino:  # 16 products per 2x2-output tile instead of 36: 256/576 of the direct MACs
-            mult = mult * 256 / 576
+                n_boards, C, 1, conv.mode]
+        mult = {"split3": 6, "fp16x2": 3}.get(conv.precision, 1)
+        if algo == "wino4":
+            from Models import board_absmax
+
+            # in_absmax is consumed by every launch: refill a work copy beside (outside)
+            # each timed launch
+            amax = board_absmax(x)
+            work = amax.clone()
+            fn = nat.lib.az_conv3x3_wino4_gpu
+            args += [nat.ptr(work), None]
+            refill = lambda: work.copy_(amax)  # noqa: E731
+            kname = (f"k_conv3x3_wino4 (az_conv3x3_wino4_gpu, Winograd F(2x2,3x3), 4 boards "
+                     f"per workgroup, {conv.precision})")
+        elif algo == "wino":
+            fn = nat.lib.az_conv3x3_wino_gpu
             kname = f"k_conv3x3_wino (az_conv3x3_wino_gpu, Winograd F(2x2,3x3), {conv.precision})"
         else:
+            fn = nat.lib.az_conv3x3_mx_gpu
             kname = f"k_conv3x3_mx (az_conv3x3_mx_gpu, {conv.precision})"
+        if algo in ("wino", "wino4"):  # 16 products per 2x2-output tile instead of 36
+            mult = mult * 256 / 576
+        args += [nat.stream_ptr()]
         peak = MFMA16_PEAK
     for _ in range(400):  # past the power-management transient (StepKernelBench.time_ms)
+        refill()
         nat.check(fn(*args), kname)
     torch.cuda.synchronize()
-    ms = launch_ms(lambda: fn(*args), 100)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(100)]
+    for e0, e1 in evs:
+        refill()  # outside the timed pair
+        e0.record()
+        fn(*args)
+        e1.record()
+    torch.cuda.synchronize()
+    ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
-    traffic = None  # HBM bytes per launch, PMC (scripts/pmc_conv.sh), for the Winograd form
+    traffic = None  # HBM bytes per launch, PMC (scripts/pmc_conv.sh), for the default form
     tj = os.path.join(ROOT, "profiles", "conv_traffic.json")
-    if "wino" in kname and conv.precision == "split3" and C == 128 and os.path.exists(tj):
+    if os.path.exists(tj):
         try:
-            traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
+            tjd = json.load(open(tj))
+            if tjd.get("kernel_tag") == f"{getattr(conv, 'algo', 'direct')}_{conv.precision}_{C}":
+                traffic = tjd.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {"kernel": kname + ", fused bias+residual+ReLU", "bound": "mfma",
@@ -262,11 +293,11 @@ def conv_roofline(sp, device, n_boards):
            "mfma_flop_per_algorithmic_flop": round(mult, 4),
            "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1)}
     if conv.precision != "fp32":
-        # every workgroup streams the whole pre-split weight set from L2 (the bound measured
-        # for this kernel: scripts/exp/wino_exp.py)
-        per_wg = (16 if getattr(conv, "algo", "direct") == "wino" else 9) * C * C * \
-            (3 if conv.precision == "split3" else 1) * 2
-        wgs = (n_boards + 1) // 2 if getattr(conv, "algo", "direct") == "wino" else n_boards
+        # every workgroup streams the whole pre-split weight set from L2
+        algo = getattr(conv, "algo", "direct")
+        per_wg = (16 if algo in ("wino", "wino4") else 9) * C * C * \
+            {"split3": 3, "fp16x2": 2}.get(conv.precision, 1) * 2
+        wgs = {"wino": (n_boards + 1) // 2, "wino4": (n_boards + 3) // 4}.get(algo, n_boards)
         out["l2_weight_stream"] = {"bytes_per_launch": per_wg * wgs,
                                    "achieved_TBps": round(per_wg * wgs / (ms * 1e-3) / 1e12, 2),
                                    "peak_TBps": L2_PEAK_TBPS}

@@ -285,7 +285,7 @@ int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* bias, const
  * wq: the weights re-laid by az_conv3x3_mx_prep_gpu from w9 [9][Co][Ci] fp32 into
  * [9][Ci/16][planes][Co][16] 16-bit words (planes = 3 for SPLIT3, 1 for FP16; 16-byte
  * aligned, 9*C*C*planes*2 bytes).  Replaces the same reference layers as az_conv3x3_gpu. */
-enum { AZ_CONV_SPLIT3 = 0, AZ_CONV_FP16 = 1 };
+enum { AZ_CONV_SPLIT3 = 0, AZ_CONV_FP16 = 1, AZ_CONV_FP16X2 = 2 };
 int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t mode,
                            void* stream);
 int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias, const float* res,
@@ -318,6 +318,9 @@ int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w, const float
  * az_conv3x3_gpu. */
 int az_conv3x3_wino_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t mode,
                              void* stream);
+/* wq size in bytes for az_conv3x3_wino_prep_gpu: 16*C*C*planes*2 (planes 3 / 1 / 2 for
+ * SPLIT3 / FP16 / FP16X2) plus, for FP16X2, 16 bytes of scale header after the words. */
+int64_t az_conv3x3_wino_prep_bytes(int32_t channels, int32_t mode);
 int az_conv3x3_wino_gpu(const float* x, const void* wq, const float* bias, const float* res,
                         float* y, int32_t n_boards, int32_t channels, int32_t relu,
                         int32_t mode, void* stream);
@@ -325,11 +328,24 @@ int az_conv3x3_wino_gpu(const float* x, const void* wq, const float* bias, const
 /* The same op, weights (az_conv3x3_wino_prep_gpu layout) and modes as az_conv3x3_wino_gpu
  * at 128 channels (csrc/conv_wino4.hip): four boards per workgroup, the transform points
  * visited row by row with the output transform folded after each row's K loop, so each
- * streamed weight fragment feeds twice the boards.  Replaces the same reference layers
- * (Models.py:72-90 ResidualBlock convs). */
+ * streamed weight fragment feeds twice the boards.  One more mode:
+ *   AZ_CONV_FP16X2 — fp32-accurate with half the products of SPLIT3: both operands as an
+ *                    fp16 pair hi + lo (22 significant bits) after exact power-of-two
+ *                    scaling (weights per layer, from az_conv3x3_wino_prep_gpu; inputs per
+ *                    board, from in_absmax), the three leading products accumulated in fp32
+ *                    and the scale removed exactly in the epilogue.
+ * in_absmax: float [n_boards] max |x| of each board (required for FP16X2, ignored
+ * otherwise; CONSUMED: the kernel resets its entries to 0).  out_absmax: NULL or float
+ * [n_boards] holding zeros: receives max |y| of each output board (the next layer's
+ * in_absmax).  Replaces the same reference layers (Models.py:72-90 ResidualBlock convs). */
 int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias, const float* res,
                          float* y, int32_t n_boards, int32_t channels, int32_t relu,
-                         int32_t mode, void* stream);
+                         int32_t mode, float* in_absmax, float* out_absmax, void* stream);
+
+/* out[b] = max |x[b][.]| over each board's 64 * channels fp32 values (NHWC): the
+ * in_absmax of az_conv3x3_wino4_gpu for a tensor no kernel produced it for. */
+int az_board_absmax_gpu(const float* x, int32_t n_boards, int32_t channels, float* out,
+                        void* stream);
 
 /* The whole residual trunk of AlphaZeroNet / FastOthelloNet in one launch
  * (csrc/conv_wino.hip): the stem (az_conv_stem_gpu's arithmetic) then n_blocks residual

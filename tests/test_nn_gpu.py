@@ -68,6 +68,7 @@ def test_bias_act_kernel_matches_torch():
 
 @pytest.mark.parametrize("kind", ["az", "fast"])
 @pytest.mark.parametrize("conv,precision,algo", [("hip", "split3", "wino"), ("hip", "split3", "wino4"),
+                                                 ("hip", "fp16x2", None),
                                                  ("hip", "split3", "direct"),
                                                  ("hip", "fp32", None), ("miopen", None, None)])
 def test_inference_copy_matches_module(kind, conv, precision, algo):
@@ -109,17 +110,21 @@ def _mx_conv(x, w, b, r, relu, mode):
     return y
 
 
-def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu"):
+def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu", out_absmax=None):
     C = x.shape[1]
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
-    planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
-    wq = torch.empty(16 * C * C * planes, dtype=torch.int16, device="cuda")
+    wq = torch.empty(nat.lib.az_conv3x3_wino_prep_bytes(C, mode) // 2, dtype=torch.int16,
+                     device="cuda")
     nat.check(nat.lib.az_conv3x3_wino_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode,
                                                nat.stream_ptr()), "az_conv3x3_wino_prep_gpu")
     y = torch.empty_like(x, memory_format=torch.channels_last)
-    nat.check(getattr(nat.lib, fn)(nat.ptr(x), nat.ptr(wq), nat.ptr(b),
-                                   None if r is None else nat.ptr(r), nat.ptr(y),
-                                   x.shape[0], C, int(relu), mode, nat.stream_ptr()), fn)
+    args = [nat.ptr(x), nat.ptr(wq), nat.ptr(b), None if r is None else nat.ptr(r), nat.ptr(y),
+            x.shape[0], C, int(relu), mode]
+    if fn == "az_conv3x3_wino4_gpu":
+        from Models import board_absmax
+
+        args += [nat.ptr(board_absmax(x)), nat.ptr(out_absmax)]
+    nat.check(getattr(nat.lib, fn)(*args, nat.stream_ptr()), fn)
     torch.cuda.synchronize()
     return y
 
@@ -208,6 +213,40 @@ def test_conv3x3_winograd4_is_fp32_accurate(B, res, relu):
     assert e_w.max() <= 2 * e_32.max() + 1e-6, (e_w.max(), e_32.max())
     assert e_w.mean() <= 2 * e_32.mean() + 1e-8, (e_w.mean(), e_32.mean())
     torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+@pytest.mark.parametrize("B", [1, 3, 5, 130, 1024])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu):
+    """FP16X2 (fp16 hi + lo operand pairs after exact power-of-two scaling, three products)
+    against fp64: the same fp32-accuracy bar as split3 (max |err| <= 2x the fp32 MFMA
+    kernel's + 1e-6, mean <= 2x), boards of very different magnitude in one batch included
+    (the input scale is per board), and the per-board max |y| output exact."""
+    C = 128
+    x, w, b, r, ref64 = _case(C, B, C * 23 + B)
+    if B > 1:  # per-board ranges from 1e-3 to 1e3
+        s = torch.logspace(-3, 3, B, device="cuda").view(B, 1, 1, 1)
+        x = (x * s).contiguous(memory_format=torch.channels_last)
+        ref64 = F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), padding=1)
+    rr = r if res else None
+    amax = torch.zeros(B, dtype=torch.float32, device="cuda")
+    y = _wino_conv(x, w, b, rr, relu, nat.AZ_CONV_FP16X2, fn="az_conv3x3_wino4_gpu",
+                   out_absmax=amax)
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    y32 = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
+                                     nat.ptr(y32), B, C, int(relu), nat.stream_ptr()), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ref = ref64 + (r.cpu().double() if res else 0)
+    if relu:
+        ref = F.relu(ref)
+    # the error bar is relative to each board's magnitude: normalise per board
+    scale = ref.abs().amax(dim=(1, 2, 3), keepdim=True).clamp_min(1e-30)
+    e_w = ((y.cpu().double() - ref).abs() / scale)
+    e_32 = ((y32.cpu().double() - ref).abs() / scale)
+    assert e_w.max() <= 2 * e_32.max() + 1e-7, (e_w.max(), e_32.max())
+    assert e_w.mean() <= 2 * e_32.mean() + 1e-9, (e_w.mean(), e_32.mean())
+    assert torch.equal(amax.cpu(), y.abs().amax(dim=(1, 2, 3)).cpu())
 
 
 def test_conv3x3_winograd4_fp16_mode():
