@@ -304,10 +304,18 @@ def conv_roofline(sp, device, n_boards):
     return out
 
 
-def cpu_baseline(net_kind, sims, seconds, seed=0):
+CALIBRATION_JSON = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+
+
+def cpu_baseline(net_kind, sims, seconds, seed=0, start_ply=0, full_games=0):
     """The oracle's restatement of one_self_play (reference algorithm, sequential MCTS,
-    batch-1 torch-CPU inference, C board oracle), timed for a bounded sample of moves of one
-    game on one core; games/s = 1 / (seconds per move x plies per game)."""
+    batch-1 torch-CPU inference, C board oracle) on one core.  The worker reaches ply
+    `start_ply` with seeded uniformly random legal moves (no search), then runs 400-sim
+    moves (fresh tree, then tree reuse as the reference does) until `seconds` are used,
+    starting over from the same ply when a game ends; games/s = 1 / (seconds per move x
+    plies per game).  full_games > 0: play that many complete games from the initial
+    position instead (the calibration against the reference pool, scripts/
+    calibrate_cpu_baseline.py)."""
     from oracle import board as ob
     from oracle.mcts import SeqMCTS
 
@@ -323,55 +331,115 @@ def cpu_baseline(net_kind, sims, seconds, seed=0):
         return p[0].numpy(), float(v[0, 0])
 
     np.random.seed(seed)
+    rng = np.random.default_rng(seed)
     a = SELFPLAY_ARGS
-    m = SeqMCTS(a["c_puct"], sims, evaluate, dirichlet_alpha=a["dirichlet_alpha"],
-                dirichlet_epsilon=a["dirichlet_epsilon"])
     game = ob.OracleGame()
-    state, player = game.get_initial_state(), 1
+
+    def opening(plies):
+        state, player = game.get_initial_state(), 1
+        for _ in range(plies):
+            valid = np.nonzero(game.get_valid_moves(state, player))[0]
+            act = int(rng.choice(valid))
+            nxt = game.get_next_state(state, act, player)
+            if game.get_value_and_terminated(nxt, act, player)[1]:
+                break
+            state, player = nxt, -player
+        return state, player
+
+    moves, games = 0, 0
     t0 = time.perf_counter()
-    moves = 0
-    while time.perf_counter() - t0 < seconds:
-        own, opp = ob.to_bitboards(state, player)
-        pi = m.search(own, opp, player, 1.0)
-        action = int(np.random.choice(65, p=pi))
-        m.make_move(action)
-        state = game.get_next_state(state, action, player)
-        moves += 1
-        if game.get_value_and_terminated(state, action, player)[1]:
+    while True:
+        m = SeqMCTS(a["c_puct"], sims, evaluate, dirichlet_alpha=a["dirichlet_alpha"],
+                    dirichlet_epsilon=a["dirichlet_epsilon"])
+        state, player = opening(0 if full_games else start_ply)
+        ply = 0 if full_games else start_ply
+        while True:
+            own, opp = ob.to_bitboards(state, player)
+            temp = a["mcts_temperature"] if ply < a["num_exploratory_moves"] else 0.0
+            pi = m.search(own, opp, player, temp)
+            action = int(np.random.choice(65, p=pi))
+            m.make_move(action)
+            state = game.get_next_state(state, action, player)
+            moves += 1
+            ply += 1
+            done = game.get_value_and_terminated(state, action, player)[1]
+            if done or (not full_games and time.perf_counter() - t0 >= seconds):
+                break
+            player = -player
+        if done:
+            games += 1
+        if full_games and games >= full_games:
             break
-        player = -player
+        if not full_games and time.perf_counter() - t0 >= seconds:
+            break
     dt = time.perf_counter() - t0
-    return {"moves": moves, "seconds": dt,
+    if full_games:
+        return {"moves": moves, "seconds": dt, "games": games, "games_per_s": games / dt}
+    return {"moves": moves, "seconds": dt, "start_ply": start_ply,
             "games_per_s": 1.0 / (dt / moves * REF_PLIES_PER_GAME)}
+
+
+def _cpu_pool(net_kind, sims, seconds, workers, full_games=0):
+    import subprocess
+
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    procs = []
+    for w in range(workers):
+        # start plies spread uniformly over a game (0, 7, 15, ..., 52 for 8 workers)
+        ply = int(w * REF_PLIES_PER_GAME / workers)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                                       net_kind, str(sims), str(seconds), str(w), str(ply),
+                                       str(full_games)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env))
+    outs = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=(seconds + 600) * 10 if not full_games else 7200)
+        if pr.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker failed ({pr.returncode})")
+        outs.append(json.loads(out.decode().strip().splitlines()[-1]))
+    return outs
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline_pool(net_kind, sims, seconds, workers):
     """cpu_baseline on `workers` host cores at once, one process each (started before any
     GPU work of theirs could exist: they hide the GPUs), like the reference's spawn-pool
-    self-play workers (train.py:220-222); games/s summed over the workers."""
-    import subprocess
-
-    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
-               ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
-                               net_kind, str(sims), str(seconds), str(w)],
-                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env)
-             for w in range(workers)]
-    outs = []
-    for pr in procs:
-        out, _ = pr.communicate(timeout=seconds * 10 + 120)
-        if pr.returncode != 0:
-            raise RuntimeError(f"cpu baseline worker failed ({pr.returncode})")
-        outs.append(json.loads(out.decode().strip().splitlines()[-1]))
+    self-play workers (train.py:220-222); worker w samples the game from ply w*60/workers,
+    so the moves cover the whole game; games/s summed over the workers.  `value` is that
+    rate times the calibration ratio measured in the build container (reference pool /
+    port on the same cores, full games: profiles/cpu_calibration.json), i.e. the port's
+    rate expressed as the reference's."""
+    outs = _cpu_pool(net_kind, sims, seconds, workers)
     moves = sum(o["moves"] for o in outs)
+    port = float(sum(o["games_per_s"] for o in outs))
+    ratio = None
+    if os.path.exists(CALIBRATION_JSON):
+        cal = json.load(open(CALIBRATION_JSON))
+        if cal.get("net") == net_kind and cal.get("sims") == sims:
+            ratio = cal.get("ratio_reference_over_port")
     net_name = "AlphaZeroNet(5,128)" if net_kind == "az5x128" else "FastOthelloNet"
-    return {"value": float(sum(o["games_per_s"] for o in outs)), "unit": "games/s",
+    return {"value": port * ratio if ratio else port, "unit": "games/s",
             "cores": workers, "kind": "port",
-            "sample": f"{workers} single-threaded worker processes, each the opening moves "
-                      f"of one self-play game (seeds 0..{workers - 1}; {moves} moves in all) "
-                      f"at {sims} sims for {seconds:.0f} s; {net_name} fp32 batch-1 torch-CPU, "
-                      f"oracle/mcts.py SeqMCTS; per worker games/s = 1/(s_per_move x "
-                      f"{REF_PLIES_PER_GAME:.0f} plies), summed",
+            "calibration_ratio": ratio, "port_value": port,
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"{workers} single-threaded worker processes; worker w plays from ply "
+                      f"w*{int(REF_PLIES_PER_GAME)}/{workers} (seeded random opening) for "
+                      f"{seconds:.0f} s of {sims}-sim moves ({moves} moves in all); "
+                      f"{net_name} fp32 batch-1 torch-CPU, oracle/mcts.py SeqMCTS; per worker "
+                      f"games/s = 1/(s_per_move x {REF_PLIES_PER_GAME:.0f} plies), summed; "
+                      + (f"value = port x calibration_ratio {ratio:.3f} (reference pool / port, "
+                         "full games, same 8 cores: profiles/cpu_calibration.json)" if ratio
+                         else "uncalibrated"),
             "per_worker_games_per_s": [round(o["games_per_s"], 5) for o in outs]}
 
 
@@ -536,6 +604,7 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":  # cpu_baseline_pool's workers
         print(json.dumps(cpu_baseline(sys.argv[2], int(sys.argv[3]), float(sys.argv[4]),
-                                      int(sys.argv[5]))), flush=True)
+                                      int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]))),
+              flush=True)
     else:
         main()

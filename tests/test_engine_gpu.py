@@ -230,3 +230,55 @@ def test_batched_selfplay_properties():
     assert len(tuples) >= 9 * 96  # the shortest possible Othello game has 9 plies
     s0, pi0, z0 = tuples[0]
     assert s0.dtype == np.int8 and s0.shape == (8, 8) and pi0.shape == (65,)
+
+
+def test_d4_augment_priors_match_reference_unsymmetrise():
+    """Fused D4 (config #5) with a NON-equivariant policy: every slot's random transform is
+    recovered from the packed leaf (an asymmetric position has 8 distinct images), and the
+    expanded children's priors must equal, bit for bit, the reference's path
+    unsymmetrise_pi(policy(random_symmetry(state))) (MCTS_model.py:15-43, :313-318)
+    followed by the mask and renormalisation of :345-349 -- restated in NumPy on the
+    reference's own (k, flip) index tables (tests/golden/d4.npz)."""
+    from mock_policy import mock_eval
+
+    d4 = load_golden("d4.npz")
+    corpus = load_golden("board_corpus.npz")
+    i = np.nonzero((corpus["game"] == 1) & (corpus["ply"] == 11))[0][0]
+    player = int(corpus["player"][i])
+    pos, neg = int(corpus["pos"][i]), int(corpus["neg"][i])
+    own, opp = own_opp(pos, neg, player)
+    w = np.uint64(1) << np.arange(64, dtype=np.uint64)
+    canon = (((np.uint64(own) & w) != 0).astype(np.int64)
+             - ((np.uint64(opp) & w) != 0).astype(np.int64))  # player * state, flat
+    images = np.stack([canon[d4["sym_board"][s]] for s in range(8)])
+    assert len({tuple(x) for x in images}) == 8  # asymmetric: the transform is identifiable
+    G = 64
+    e = Engine(G, 1, d4_augment=True, auto_play=False, seed=11)
+    for s in range(G):
+        e.set_root(s, own, opp, player)
+    e.begin_search(-1, 1)
+    e.select()
+    planes = np.rint(e.nn_in.cpu().numpy()).astype(np.int64)
+    syms = [int(np.nonzero((images == planes[g]).all(1))[0][0]) for g in range(G)]
+    assert len(set(syms)) == 8  # every D4 element drawn somewhere
+    pr, va = mock_eval_torch(e.nn_in)  # position-dependent: not D4-equivariant
+    e.priors.copy_(pr)
+    e.values.copy_(va)
+    e.expand()
+    valid = np.zeros(65, np.uint8)
+    legal = nat.legal_cpu(np.array([own], np.uint64), np.array([opp], np.uint64))[0]
+    valid[:64] = ((np.uint64(legal) >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(np.uint8)
+    if legal == 0:
+        valid[64] = 1
+    for g in range(G):
+        p_sym, _ = mock_eval(images[syms[g]])  # the policy on the transformed board
+        priors = p_sym[d4["sym_unpi"][syms[g]]]  # unsymmetrise_pi
+        priors = priors * valid  # float32 * uint8 -> float32 (NEP 50)
+        tot = priors.sum()
+        if tot > 1e-12:
+            priors = priors / tot
+        t = e.export_tree(g)
+        fc, nc = int(t["first"][0]), int(t["nchild"][0])
+        acts = t["action"][fc:fc + nc].astype(np.int64)
+        assert (acts == np.nonzero(valid)[0]).all()
+        assert (t["prior"][fc:fc + nc].astype(np.float32) == priors[acts]).all(), g
