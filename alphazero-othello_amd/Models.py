@@ -343,15 +343,16 @@ class _HipStem(nn.Module):
         self.w9 = nn.Parameter(w.reshape(w.shape[0], 9).t().contiguous(), requires_grad=False)
         self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
 
-    def forward(self, x, res=None, relu=True):
+    def forward(self, x, res=None, relu=True, absmax=None):
+        """absmax: optional float [B] receiving each board's max |y| (FP16X2 trunk)."""
         import az_native as nat
 
         planes = x.reshape(x.shape[0], 64).contiguous()
         y = torch.empty((x.shape[0], self.channels, 8, 8), dtype=torch.float32, device=x.device,
                         memory_format=torch.channels_last)
-        nat.check(nat.lib.az_conv_stem_gpu(nat.ptr(planes), nat.ptr(self.w9), nat.ptr(self.bias),
-                                           nat.ptr(y), x.shape[0], self.channels,
-                                           nat.stream_ptr()), "az_conv_stem_gpu")
+        nat.check(nat.lib.az_conv_stem2_gpu(nat.ptr(planes), nat.ptr(self.w9), nat.ptr(self.bias),
+                                            nat.ptr(y), x.shape[0], self.channels,
+                                            nat.ptr(absmax), nat.stream_ptr()), "az_conv_stem2_gpu")
         return y
 
 
@@ -458,21 +459,26 @@ class FusedInferenceNet(nn.Module, Inference):
             planes = x.reshape(x.shape[0], 64).contiguous()
             h = c2s[0].forward_stem(planes, self.stem, 2, x=c1s[0].forward_stem(planes, self.stem, 1))
             c1s, c2s = c1s[1:], c2s[1:]
-        else:
-            h = self.stem(x)
-        if c1s and getattr(c1s[0], "precision", "") == "fp16x2":
+        elif c1s and getattr(c1s[0], "precision", "") == "fp16x2":
             # per-board input ranges ping-pong between two buffers: each conv consumes (and
-            # resets) one and accumulates its output's into the other
-            B = h.shape[0]
+            # resets) one and accumulates its output's into the other; the stem writes the
+            # first (or, for a non-HIP stem, a separate max pass does)
+            B = x.shape[0]
             bufs = getattr(self, "_absmax", None)
-            if bufs is None or bufs[0].shape[0] != B or bufs[0].device != h.device:
-                bufs = self._absmax = [torch.zeros(B, dtype=torch.float32, device=h.device)
+            if bufs is None or bufs[0].shape[0] != B or bufs[0].device != x.device:
+                bufs = self._absmax = [torch.zeros(B, dtype=torch.float32, device=x.device)
                                        for _ in range(2)]
-            board_absmax(h, out=bufs[0])
+            if isinstance(self.stem, _HipStem):
+                h = self.stem(x, absmax=bufs[0])
+            else:
+                h = self.stem(x)
+                board_absmax(h, out=bufs[0])
             for c1, c2 in zip(c1s, c2s):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1])
                 h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0])
             return h
+        else:
+            h = self.stem(x)
         for c1, c2 in zip(c1s, c2s):
             h = c2(c1(h), res=h)
         return h

@@ -107,6 +107,7 @@ SIGNATURES = {
     "az_bias_act_gpu": [_P, _P, _P, _I64, _I32, _I32, _P],
     "az_conv3x3_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P],
     "az_conv_stem_gpu": [_P, _P, _P, _P, _I32, _I32, _P],
+    "az_conv_stem2_gpu": [_P, _P, _P, _P, _I32, _I32, _P, _P],
     "az_conv3x3_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_prep_gpu": [_P, _P, _I32, _I32, _P],
     "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],

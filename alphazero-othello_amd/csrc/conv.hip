@@ -189,7 +189,9 @@ template <int CO>
 __global__ __launch_bounds__(256) void k_conv_stem(const float* __restrict__ planes,
                                                    const float* __restrict__ w,
                                                    const float* __restrict__ bias,
-                                                   float* __restrict__ y, int64_t n_boards) {
+                                                   float* __restrict__ y, int64_t n_boards,
+                                                   float* __restrict__ absmax) {
+  __shared__ float s_max[4];
   constexpr int G4 = CO / 4;            // float4 channel groups per position
   constexpr int PPI = 256 / G4;         // positions per pass of the workgroup
   __shared__ float s_pl[64];
@@ -204,6 +206,7 @@ __global__ __launch_bounds__(256) void k_conv_stem(const float* __restrict__ pla
     if (tid < 64) s_pl[tid] = planes[b * 64 + tid];
     __syncthreads();
     float4* out = reinterpret_cast<float4*>(y + b * 64 * CO);
+    float bmax = 0.0f;
 #pragma unroll
     for (int p0 = 0; p0 < 64; p0 += PPI) {
       const int p = p0 + tid / G4, py = p >> 3, px = p & 7;
@@ -224,6 +227,14 @@ __global__ __launch_bounds__(256) void k_conv_stem(const float* __restrict__ pla
       acc.z = fmaxf(acc.z, 0.f);
       acc.w = fmaxf(acc.w, 0.f);
       out[p * G4 + co / 4] = acc;
+      bmax = fmaxf(bmax, fmaxf(fmaxf(acc.x, acc.y), fmaxf(acc.z, acc.w)));
+    }
+    if (absmax) {  // the board's max |y| (outputs are >= 0 after the ReLU)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, off, 64));
+      if ((tid & 63) == 0) s_max[tid >> 6] = bmax;
+      __syncthreads();
+      if (tid == 0) absmax[b] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
     }
   }
 }
@@ -316,6 +327,12 @@ extern "C" int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* 
 
 extern "C" int az_conv_stem_gpu(const float* planes, const float* w9, const float* bias,
                                 float* y, int32_t n_boards, int32_t channels, void* stream) {
+  return az_conv_stem2_gpu(planes, w9, bias, y, n_boards, channels, nullptr, stream);
+}
+
+extern "C" int az_conv_stem2_gpu(const float* planes, const float* w9, const float* bias,
+                                 float* y, int32_t n_boards, int32_t channels, float* absmax,
+                                 void* stream) {
   AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv_stem_gpu: n_boards < 0");
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(planes && w9 && bias && y, AZ_ERR_ARG, "az_conv_stem_gpu: null buffer");
@@ -323,10 +340,10 @@ extern "C" int az_conv_stem_gpu(const float* planes, const float* w9, const floa
   const int64_t blocks = n_boards < 8192 ? n_boards : 8192;  // one board per workgroup pass
   if (channels == 128)
     hipLaunchKernelGGL(k_conv_stem<128>, dim3((unsigned)blocks), dim3(256), 0, s, planes, w9,
-                       bias, y, (int64_t)n_boards);
+                       bias, y, (int64_t)n_boards, absmax);
   else if (channels == 64)
     hipLaunchKernelGGL(k_conv_stem<64>, dim3((unsigned)blocks), dim3(256), 0, s, planes, w9,
-                       bias, y, (int64_t)n_boards);
+                       bias, y, (int64_t)n_boards, absmax);
   else
     return azc::set_error(AZ_ERR_ARG, "az_conv_stem_gpu: channels must be 64 or 128");
   AZ_HIP(hipGetLastError());

@@ -394,6 +394,10 @@ int az_heads_az_gpu(const float* h, const float* wpv, const float* bpv, const fl
  * 186-187). */
 int az_conv_stem_gpu(const float* planes, const float* w9, const float* bias, float* y,
                      int32_t n_boards, int32_t channels, void* stream);
+/* the same with each board's max |y| written to absmax[b] (NULL: not computed): the
+ * in_absmax of the first trunk conv in FP16X2 mode (az_conv3x3_wino4_gpu) */
+int az_conv_stem2_gpu(const float* planes, const float* w9, const float* bias, float* y,
+                      int32_t n_boards, int32_t channels, float* absmax, void* stream);
 
 #ifdef __cplusplus
 }

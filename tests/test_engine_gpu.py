@@ -272,7 +272,8 @@ def test_d4_augment_priors_match_reference_unsymmetrise():
         valid[64] = 1
     for g in range(G):
         p_sym, _ = mock_eval(images[syms[g]])  # the policy on the transformed board
-        priors = p_sym[d4["sym_unpi"][syms[g]]]  # unsymmetrise_pi
+        # unsymmetrise_pi of arange(65) (float64 in the fixture) is the gather index map
+        priors = p_sym[d4["sym_unpi"][syms[g]].astype(np.int64)]
         priors = priors * valid  # float32 * uint8 -> float32 (NEP 50)
         tot = priors.sum()
         if tot > 1e-12:

@@ -51,6 +51,14 @@ def test_stem_kernel_matches_torch(C):
                                        C, nat.stream_ptr()), "az_conv_stem_gpu")
     torch.cuda.synchronize()
     torch.testing.assert_close(y, ref, **TOL)
+    # the absmax-fused entry: same output bit for bit, plus each board's exact max |y|
+    y2 = torch.empty_like(y, memory_format=torch.channels_last)
+    amax = torch.full((37,), -1.0, device="cuda")
+    nat.check(nat.lib.az_conv_stem2_gpu(nat.ptr(planes), nat.ptr(w9), nat.ptr(b), nat.ptr(y2), 37,
+                                        C, nat.ptr(amax), nat.stream_ptr()), "az_conv_stem2_gpu")
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y)
+    assert torch.equal(amax, y.abs().amax(dim=(1, 2, 3)))
 
 
 def test_bias_act_kernel_matches_torch():
