@@ -1,10 +1,13 @@
 """Policy/value networks with the reference's module names and state_dict keys
 (reference Models.py:1-221), plus the batched device-side evaluation the engine uses.
 
-The nets are plain PyTorch-ROCm (MIOpen convolutions / hipBLASLt linears on MFMA): the
-only dense contractions on the path.  `Inference.inference` keeps the reference's batch-1
-host API (Models.py:11-31); `evaluate_planes` is what the batched self-play engine calls
-on the [G, 64] canonical planes it packs on device.
+The modules are plain PyTorch (they carry the reference's state_dict keys and are the fp32
+bar the tests hold the device path to).  What the engine evaluates is `inference_copy`: a
+`FusedInferenceNet` whose stem, residual trunk (the Winograd / direct MFMA conv kernels of
+csrc/conv*.hip) and heads (csrc/heads.hip) are this library's own HIP kernels.
+`Inference.inference` keeps the reference's batch-1 host API (Models.py:11-31);
+`evaluate_planes` is what the batched self-play engine calls on the [G, 64] canonical
+planes it packs on device.
 """
 import os
 from typing import Tuple

@@ -45,14 +45,16 @@ def main():
         r = torch.randn_like(x).relu().contiguous(memory_format=torch.channels_last)
         amax = board_absmax(x)
         base = None
-        for name, mname in CASES:
+        cases = [(n, m, True) for n, m in CASES]
+        cases += [(n, m, False) for n, m in CASES if "wino4" in n]  # also without residual
+        for name, mname, with_res in cases:
             if only and only not in name:
                 continue
             mode = MODES[mname]
             y = torch.empty_like(x)
             fn = getattr(nat.lib, name)
             args = [nat.ptr(x), nat.ptr(wq[("direct" if "mx" in name else "wino", mname)]),
-                    nat.ptr(bias), nat.ptr(r), nat.ptr(y), B, C, 1, mode]
+                    nat.ptr(bias), nat.ptr(r) if with_res else None, nat.ptr(y), B, C, 1, mode]
             if "wino4" in name:
                 # fp16x2 consumes in_absmax: give every launch a fresh copy (a device copy
                 # beside the timed kernel, the same in every timed launch)
@@ -78,10 +80,12 @@ def main():
                 e1.record()
             torch.cuda.synchronize()
             ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
+            if not with_res:
+                y = y + r  # compare the residual-free form on the same footing (ReLU aside)
             if base is None:
                 base = y.clone()
             flop = 2.0 * B * 64 * C * C * 9
-            print(json.dumps({"kernel": name, "mode": mname, "boards": B,
+            print(json.dumps({"kernel": name, "mode": mname, "boards": B, "residual": with_res,
                               "avg_launch_us": round(ms * 1e3, 2),
                               "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1),
                               "max_abs_diff_vs_first": float((y - base).abs().max())}),
