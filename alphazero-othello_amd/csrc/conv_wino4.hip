@@ -113,7 +113,14 @@ struct W4 {
   // window read never needs a mask: [board][10][10][16 ch] fp32
   static constexpr int IN_ROW = 10 * 64, IN_BOARD = 10 * IN_ROW, IN_SLOT = BOARDS * IN_BOARD;
   static constexpr int IN_OFF = 2 * BUF;             // two slots after the V double buffer
-  static constexpr int LDS_BYTES = 2 * BUF + 2 * IN_SLOT;
+  // residual half (RES kernels): output rows 2ty + I of the 4 boards, [board][ty][8][C] fp32,
+  // staged during group 2 + I and added by that half's epilogue
+  static constexpr int RES_OFF = 2 * BUF + 2 * IN_SLOT, RES_BYTES = BOARDS * 4 * 8 * C * 4;
+  static constexpr int RS = RES_BYTES / 16 / THREADS / 8;  // 16-byte pieces per thread per chunk
+  // staged only where it fits beside the rest (not split3's three planes: its residual is
+  // read from global memory in the epilogue)
+  static constexpr bool RES_FITS = RES_OFF + RES_BYTES <= 160 * 1024;
+  static constexpr int LDS_BYTES = RES_FITS ? RES_OFF + RES_BYTES : RES_OFF;
   static constexpr int LD_PER_THREAD = BOARDS * 64 * 4 / THREADS;  // 16-byte loads per chunk
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes of one (chunk, point)
   static constexpr int CHUNKS = C / 16;
@@ -328,16 +335,48 @@ struct St {
   f32x16 Y[2][2][G::NRT];
   int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], soff[G::TPT], aoff[G::NRT];
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
-  int wlane;
+  int wlane, tid, b0, nb;
+  unsigned lds_res;   // LDS byte address of this wave's first residual piece
   const float* x;
+  const float* res;
   const char* wq;
   char* lds;
 };
 
+// one 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane i's 16 bytes land at LDS
+// byte address lds_dst + 16 i.  Issued as asm so the compiler's vmcnt bookkeeping for the
+// weight and input loads is not collapsed to vmcnt(0) around it; its completion is waited
+// for explicitly (vmcnt(0)) before the barrier that precedes the reads
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst));
+}
+
+__device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// residual staging: piece p = (c * RS + s) * THREADS + tid of half I (16 bytes; 256 pieces
+// = one 4 KiB [8 positions][C] row segment seg = p / 256 = (board, ty)), DMA'd at chunk c's
+// second step straight into LDS (linear: offset 16 p)
+template <class G, int I>
+__device__ __forceinline__ void res_dma(St<G>& S, int c) {
+#pragma unroll
+  for (int s = 0; s < G::RS; ++s) {
+    const int p = (c * G::RS + s) * G::THREADS + S.tid, seg = p >> 8, w = p & 255;
+    const int bd = seg >> 2, ty = seg & 3, bs = bd < S.nb ? bd : S.nb - 1;
+    glds16(S.res + ((size_t)(S.b0 + bs) * 64 + (2 * ty + I) * 8) * G::C + 4 * w,
+           __builtin_amdgcn_readfirstlane(S.lds_res + 16 * (c * G::RS + s) * G::THREADS));
+  }
+}
+
 // one chunk L (of parity PAR, so a step's weight ring slot is a compile-time constant): its
 // four steps, the next chunk's transform into the other LDS buffer, the windows of the
 // chunk after that requested
-template <class G, int PAR>
+template <class G, int PAR, int STAGE>
 __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
   const char* cur = S.lds + (L & 1) * G::BUF;
   char* nxt = S.lds + ((L + 1) & 1) * G::BUF;
@@ -372,6 +411,9 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
     // the chunk-after-next's input slice at the chunk's first step: four steps of latency
     // cover before it is stored to LDS at the chunk's end
     if (l == 0 && !(AZ_W4_EXP & 2)) load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
+    if constexpr (STAGE >= 0) {
+      if (l == 1) res_dma<G, STAGE>(S, L & 7);
+    }
 #pragma unroll
     for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
       if (l == 0) put_point<G, 0>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
@@ -417,16 +459,55 @@ __device__ __forceinline__ void zero_acc(St<G>& S) {
       for (int e = 0; e < 16; ++e) S.acc[l][t][e] = 0.0f;
 }
 
-// transform-grid row K (compile time): its eight chunks, then the fold
-template <class G, int K>
+// transform-grid row K (compile time): its eight chunks (staging residual half STAGE, or
+// none for -1), then the fold
+template <class G, int K, int STAGE = -1>
 __device__ __forceinline__ void run_group(St<G>& S) {
 #pragma unroll 1
   for (int c = 0; c < G::CHUNKS; c += 2) {
-    run_chunk<G, 0>(S, K * G::CHUNKS + c);
-    run_chunk<G, 1>(S, K * G::CHUNKS + c + 1);
+    run_chunk<G, 0, STAGE>(S, K * G::CHUNKS + c);
+    run_chunk<G, 1, STAGE>(S, K * G::CHUNKS + c + 1);
   }
   fold<G, K>(S.acc, S.Y);
   zero_acc<G>(S);
+}
+
+template <class G>
+struct Epi {
+  float unsc[2 * G::NRT];  // per board of the wave's row tiles: tile 32t + ... -> 2t + (e >= 8)
+  float bmax[2 * G::NRT];
+  float bv;
+  int co;
+};
+
+// output half I (rows 2ty + I): accumulator element e of row tile rt = tile 32rt + (e&3) +
+// 8(e>>2) + 4h, column co; Y[I][j] = output (2ty + I, 2tx + j); + bias (+ the staged
+// residual), ReLU, store, and the boards' max |y|
+template <class G, int I, bool RES, bool RELU>
+__device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __restrict__ res,
+                                         float* __restrict__ y, int rt0, int h) {
+  constexpr int C = G::C;
+#pragma unroll
+  for (int t = 0; t < G::NRT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int T = 32 * (rt0 + t) + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
+      if (bd >= S.nb) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pos = (2 * ty + I) * 8 + 2 * tx + j;
+        float v = (G::SCALED ? S.Y[I][j][t][e] * E.unsc[2 * t + (e >> 3)] : S.Y[I][j][t][e]) + E.bv;
+        if (RES && G::RES_FITS)
+          v += *reinterpret_cast<const float*>(
+              S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx + j) * C + E.co) * 4);
+        else if (RES)
+          v += res[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co];
+        if (RELU) v = fmaxf(v, 0.0f);
+        y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
+        E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fabsf(v));
+      }
+    }
 }
 
 template <class G, bool RES, bool RELU>
@@ -441,6 +522,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   S.lds = reinterpret_cast<char*>(lds4);
   S.x = x;
   S.wq = wq;
+  S.res = res;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -449,6 +531,10 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   const int col0 = 32 * cb;
   const int b0 = blockIdx.x * G::BOARDS;
   const int nb = n_boards - b0 < G::BOARDS ? n_boards - b0 : G::BOARDS;
+  S.tid = tid;
+  S.b0 = b0;
+  S.nb = nb;
+  S.lds_res = (unsigned)(uintptr_t)(S.lds + G::RES_OFF) + 16 * 64 * wave;
   S.wlane = (col0 + r) * 32 + h * 16;
 #pragma unroll
   for (int t = 0; t < G::NRT; ++t)
@@ -517,59 +603,46 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u)
     read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], 1);
-  W4_STAMP(1);
-  run_group<G, 0>(S);
-  W4_STAMP(2);
-  run_group<G, 1>(S);
-  W4_STAMP(3);
-  run_group<G, 2>(S);
-  W4_STAMP(4);
-  run_group<G, 3>(S);
-  W4_STAMP(5);
-
-  // ---- epilogue: accumulator element e of row tile rt = tile 32rt + (e&3) + 8(e>>2) + 4h,
-  // column col0 + r; Y[i][j] = output (2ty + i, 2tx + j)
-  const int co = col0 + r;
-  const float bv = bias[co];
-  // FP16X2: M carries 2^(su + sv_board); removing it is an exact power-of-two product
-  float unsc[2 * G::NRT];  // per board of this wave's row tiles: tile 32t + ... -> 2t + (e >= 8)
+  // epilogue constants: bias, and (FP16X2) the scale M carries, 2^(su + sv_board); removing
+  // it is an exact power-of-two product
+  Epi<G> E;
+  E.co = col0 + r;
+  E.bv = bias[E.co];
 #pragma unroll
-  for (int i = 0; i < 2 * G::NRT; ++i) unsc[i] = 1.0f;
+  for (int i = 0; i < 2 * G::NRT; ++i) {
+    E.unsc[i] = 1.0f;
+    E.bmax[i] = 0.0f;
+  }
   if constexpr (G::SCALED) {
     const int su = reinterpret_cast<const int*>(wq + (size_t)G::QSTEPS * G::STEP_BYTES)[1];
 #pragma unroll
     for (int i = 0; i < 2 * G::NRT; ++i) {
       const int bd = 2 * rt0 + i;
       const int e = frexp_exp(bd < nb ? in_absmax[b0 + bd] : 0.0f);
-      unsc[i] = ldexpf(1.0f, -(su + 13 - e));
+      E.unsc[i] = ldexpf(1.0f, -(su + 13 - e));
     }
   }
-  float bmax[2 * G::NRT];
-#pragma unroll
-  for (int i = 0; i < 2 * G::NRT; ++i) bmax[i] = 0.0f;
-#pragma unroll
-  for (int t = 0; t < G::NRT; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int T = 32 * (rt0 + t) + (e & 3) + 8 * (e >> 2) + 4 * h;
-      const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-      if (bd >= nb) continue;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const size_t o = ((size_t)(b0 + bd) * 64 + (2 * ty + i) * 8 + 2 * tx + j) * C + co;
-          float v = (G::SCALED ? S.Y[i][j][t][e] * unsc[2 * t + (e >> 3)] : S.Y[i][j][t][e]) + bv;
-          if (RES) v += res[o];
-          if (RELU) v = fmaxf(v, 0.0f);
-          y[o] = v;
-          bmax[2 * t + (e >> 3)] = fmaxf(bmax[2 * t + (e >> 3)], fabsf(v));
-        }
-    }
+  W4_STAMP(1);
+  run_group<G, 0>(S);
+  W4_STAMP(2);
+  run_group<G, 1>(S);
+  W4_STAMP(3);
+  // output rows 2ty (Y[0]) are final after group 2: stored while group 3 computes, with
+  // their residual staged through LDS during group 2 (and the odd rows' during group 3)
+  constexpr bool STAGED = RES && G::RES_FITS;
+  run_group<G, 2, STAGED ? 0 : -1>(S);
+  W4_STAMP(4);
+  if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
+  epilogue<G, 0, RES, RELU>(S, E, res, y, rt0, h);
+  if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
+  run_group<G, 3, STAGED ? 1 : -1>(S);
+  W4_STAMP(5);
+  if (STAGED) vm_barrier();
+  epilogue<G, 1, RES, RELU>(S, E, res, y, rt0, h);
   if (out_absmax) {  // the next layer's in_absmax: one atomic per (wave, board)
 #pragma unroll
     for (int i = 0; i < 2 * G::NRT; ++i) {
-      float m = bmax[i];
+      float m = E.bmax[i];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
       const int bd = 2 * rt0 + i;
