@@ -184,27 +184,65 @@ AZ_HD uint64_t legal(uint64_t own, uint64_t opp) {
 // Up-rays (towards higher bit indices, `sq` excluded) of the four lines through a square:
 // k = 0 row (+1), 1 column (+8), 2 diagonal (+9), 3 anti-diagonal (+7).  The down-rays of
 // sq are the up-rays of 63 - sq on the rotated board (rev64).
-AZ_HD uint64_t ray_up(int sq, int k) {
-  const int dr[4] = {0, 1, 1, 1}, dc[4] = {1, 0, 1, -1};
+constexpr uint64_t ray_up(int sq, int k) {
+  const int dr = k == 0 ? 0 : 1, dc = k == 0 ? 1 : (k == 1 ? 0 : (k == 2 ? 1 : -1));
   uint64_t m = 0;
-  int r = (sq >> 3) + dr[k], c = (sq & 7) + dc[k];
+  int r = (sq >> 3) + dr, c = (sq & 7) + dc;
   while (r < 8 && c >= 0 && c < 8) {
     m |= 1ull << (r * 8 + c);
-    r += dr[k];
-    c += dc[k];
+    r += dr;
+    c += dc;
   }
   return m;
 }
 
+// The whole [64][4] up-ray table, built at compile time (kernels copy it into LDS with one
+// load per thread instead of running ray_up's loop per block).
+struct RayTable {
+  uint64_t r[64 * 4];
+  constexpr RayTable() : r{} {
+    for (int i = 0; i < 64 * 4; ++i) r[i] = ray_up(i >> 2, i & 3);
+  }
+};
+
+// bop3 with the third operand one 32-bit word applied to both halves (a sign mask).
+template <uint8_t T>
+AZ_HD uint64_t bop3_w(uint64_t a, uint64_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, c, T);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), c, T);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return bop3<T>(a, b, ((uint64_t)c << 32) | c);
+#endif
+}
+
+// x - 1 as one v_lshl_add_u64 on a register pair (left alone, the compiler forms it from
+// the two halves bop3 produced with an extra 32-bit add)
+AZ_HD uint64_t dec64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) && AZ_SHIFT_ASM
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, -1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x - 1ull;
+#endif
+}
+
 // Stones of `opp` captured along one up-ray R by a stone placed below it: the run of
 // opponent stones up to the first non-opponent square x, kept only if x holds an own stone.
+// x = lowbit(o) with o = R & ~opp; xo = x if it is own, else 0; e = xo - 1 is then the
+// squares below x, or all ones when xo = 0 — the only case with the sign bit set (x is at
+// most bit 63), so the sign mask of e's high word drops it: 9 VALU per ray, no compare or
+// select.
 AZ_HD uint64_t ray_flips(uint64_t R, uint64_t own, uint64_t opp) {
   using namespace tt;
   const uint64_t o = R & ~opp;                     // non-opponent squares of the ray
   const uint64_t d = o - 1ull;                     // bits below the first of them set
-  const uint64_t run = bop3<A & B & ~C>(R, d, o);  // the ray below x: all opponent stones
   const uint64_t xo = bop3<A & ~B & C>(o, d, own); // x itself, if it holds an own stone
-  return xo ? run : 0ull;
+  const uint64_t e = dec64(xo);
+  const uint32_t neg = (uint32_t)((int32_t)(uint32_t)(e >> 32) >> 31);
+  return bop3_w<A & B & ~C>(R, e, neg);
 }
 
 // flips() from ray tables: `up` = the four up-rays of sq, `upr` = those of 63 - sq;

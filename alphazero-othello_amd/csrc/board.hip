@@ -32,6 +32,7 @@ int set_error(int code, const char* fmt, ...) {
 namespace {
 
 constexpr int kBlock = 256;
+__constant__ const azb::RayTable kRays;
 static_assert(kBlock == 64 * 4, "k_step stages one up-ray per thread");
 
 // The board step of one position (the body of both k_step forms): branch-free make-move
@@ -63,6 +64,41 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // 8-byte, write-back form below.  Needs 16-byte aligned own/opp/out arrays, a 2-byte
 // aligned act and a 4-byte aligned status array (the host checks); an odd n leaves the
 // last position to the lane whose pair is half live.
+// Grid cap of k_step2: 256 CUs x 64 blocks, i.e. two grid-stride iterations per lane at
+// 2^24 positions.  Same-box A/B (scripts/step_ab.py): 0.1268 ms at 16,384 blocks against
+// 0.1319 at 8,192, 0.1277 at 32,768 (one iteration), 0.146 at 2,048 (all resident, 16
+// iterations); requesting the next iteration's inputs before the current compute
+// (software prefetch) measured no gain at 8,192 and a loss at 16,384 (0.1303).
+#ifndef AZ_STEP_GRID_CAP
+#define AZ_STEP_GRID_CAP (256 * 64)
+#endif
+
+// one lane's pair of inputs (a = own, b = opp, c = the two actions)
+struct PairIn {
+  u64x2 a, b;
+  uint32_t c;
+};
+
+__device__ __forceinline__ PairIn load_pair(const char* own_b, const char* opp_b,
+                                            const uint8_t* act, uint32_t j, uint32_t pairs,
+                                            uint32_t full) {
+  PairIn in;
+  in.a = {0ull, 0ull};
+  in.b = {0ull, 0ull};
+  in.c = azb::kPass | (azb::kPass << 8);
+  const uint32_t o16 = j * 16u;
+  if (j < full) {
+    in.a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(own_b + o16));
+    in.b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(opp_b + o16));
+    in.c = *reinterpret_cast<const uint16_t*>(act + 2u * j);
+  } else if (j < pairs) {  // odd n: the last position alone
+    in.a.x = *reinterpret_cast<const uint64_t*>(own_b + o16);
+    in.b.x = *reinterpret_cast<const uint64_t*>(opp_b + o16);
+    in.c = act[2u * j] | (azb::kPass << 8);
+  }
+  return in;
+}
+
 __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ own,
                                                   const uint64_t* __restrict__ opp,
                                                   const uint8_t* __restrict__ act,
@@ -72,32 +108,22 @@ __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ o
                                                   uint16_t* __restrict__ status_o,
                                                   uint32_t n) {
   __shared__ __align__(16) uint64_t rays[64 * 4];
-  rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
-  __syncthreads();
+  rays[threadIdx.x] = kRays.r[threadIdx.x];
   const azb::WaveLane L = azb::wave_lane();
   const uint32_t pairs = (n + 1) / 2, full = n / 2;
   const uint32_t stride = gridDim.x * kBlock;
   const uint32_t p_pad = (pairs + kBlock - 1) / kBlock * kBlock;
   const char* own_b = reinterpret_cast<const char*>(own);
   const char* opp_b = reinterpret_cast<const char*>(opp);
+  __syncthreads();
   for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < p_pad; j += stride) {
-    const uint32_t o16 = j * 16u;
-    u64x2 a = {0ull, 0ull}, b = {0ull, 0ull};
-    uint32_t c = azb::kPass | (azb::kPass << 8);
+    const PairIn cur = load_pair(own_b, opp_b, act, j, pairs, full);
     const bool live0 = j < pairs, live1 = j < full;
-    if (live1) {
-      a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(own_b + o16));
-      b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(opp_b + o16));
-      c = *reinterpret_cast<const uint16_t*>(act + 2u * j);
-    } else if (live0) {  // odd n: the last position alone
-      a.x = *reinterpret_cast<const uint64_t*>(own_b + o16);
-      b.x = *reinterpret_cast<const uint64_t*>(opp_b + o16);
-      c = act[2u * j] | (azb::kPass << 8);
-    }
     uint64_t o0, p0, l0, o1, p1, l1;
     uint16_t s0, s1;
-    step_one(rays, L, a.x, b.x, c & 0xFF, live0, o0, p0, l0, s0);
-    step_one(rays, L, a.y, b.y, c >> 8, live1, o1, p1, l1, s1);
+    step_one(rays, L, cur.a.x, cur.b.x, cur.c & 0xFF, live0, o0, p0, l0, s0);
+    step_one(rays, L, cur.a.y, cur.b.y, cur.c >> 8, live1, o1, p1, l1, s1);
+    const uint32_t o16 = j * 16u;
     char* oo = reinterpret_cast<char*>(own_o) + o16;
     char* po = reinterpret_cast<char*>(opp_o) + o16;
     char* lo = reinterpret_cast<char*>(legal_o) + o16;
@@ -128,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ ow
                                                  uint16_t* __restrict__ status_o,
                                                  uint32_t n) {
   __shared__ __align__(16) uint64_t rays[64 * 4];
-  rays[threadIdx.x] = azb::ray_up(threadIdx.x >> 2, threadIdx.x & 3);
+  rays[threadIdx.x] = kRays.r[threadIdx.x];
   __syncthreads();
   const azb::WaveLane L = azb::wave_lane();
   // every lane runs the same number of iterations (the terminal check is wave-cooperative)
@@ -185,10 +211,10 @@ const uint64_t* host_rays() {
   return table.r;
 }
 
-unsigned grid_for(int64_t n) {
-  // enough waves to cover the chip many times over; grid-stride for the rest
+unsigned grid_for(int64_t n, int64_t cap = 256 * 32) {
+  // enough waves to cover the chip many times over (256 CUs x 32 blocks); grid-stride for
+  // the rest
   const int64_t blocks = (n + kBlock - 1) / kBlock;
-  const int64_t cap = 256 * 32;  // 256 CUs x 32 blocks
   return (unsigned)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
 }
 
@@ -322,7 +348,7 @@ int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
                       (reinterpret_cast<uintptr_t>(act) & 1u) == 0 &&
                       (reinterpret_cast<uintptr_t>(status_o) & 3u) == 0;
   if (paired)
-    hipLaunchKernelGGL(k_step2, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_step2, dim3(grid_for((n + 1) / 2, AZ_STEP_GRID_CAP)), dim3(kBlock), 0,
                        azc::as_stream(stream), own, opp, act, own_o, opp_o, legal_o, status_o,
                        (uint32_t)n);
   else

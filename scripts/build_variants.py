@@ -18,7 +18,13 @@ def build(name, extra):
     want = az_build.source_hash()
     flags = [f for f in az_build.FLAGS if f != "-shared"] + extra.split()
     objs = []
+    only = os.environ.get("ONLY")  # e.g. ONLY=board.hip: the rest from az_build's object cache
+    cached = []
     for src in az_build.SOURCES:
+        if only and os.path.basename(src) not in only.split(","):
+            objs.append(az_build._object(src, want, "/opt/rocm/bin/hipcc", False))
+            cached.append(objs[-1])
+            continue
         obj = os.path.join(out, os.path.basename(src) + ".o")
         subprocess.check_call(["/opt/rocm/bin/hipcc"] + flags + [f'-DAZ_BUILD_ID="{want}"', "-c",
                                os.path.join(az_build.HERE, src), "-o", obj])
@@ -26,7 +32,8 @@ def build(name, extra):
     subprocess.check_call(["/opt/rocm/bin/hipcc"] + az_build.FLAGS + objs +
                           ["-o", os.path.join(out, "libaz_othello.so")])
     for o in objs:
-        os.remove(o)
+        if o not in cached:
+            os.remove(o)
     return name
 
 
