@@ -220,18 +220,31 @@ __device__ __forceinline__ void store_in(char* slot, const f32x4 (&ld)[G::LD_PER
   for (int j = 0; j < G::LD_PER_THREAD; ++j) *reinterpret_cast<f32x4*>(slot + ldst[j]) = ld[j];
 }
 
+// Column slot of padded column c (0..9) in a slot row: c ^ (c>>1 & 1) ^ (c>>2 & 1) << 1.  A
+// half-wave's window reads hit columns {b, b+2, b+4, b+6} of one row (four tiles), 64 B
+// each, and the compiler pairs the two window rows into ds_read2_b64 (16-lane groups, banks
+// (a/4) mod 32: columns c, c+2 meet).  Unpermuted, c and c + 2 (ds_read2_b64) or c and
+// c + 4 (ds_read_b64, banks (a/4) mod 64) share banks; here c, c+2 differ in 64-B parity and
+// {b, b+2, b+4, b+6} are distinct mod 4, so both forms are conflict-free.  The input stores
+// (ds_write_b128, 8-lane groups, (a/4) mod 32) pair positions (c, c+2) to match (the load
+// lane order below); SQ_LDS_BANK_CONFLICT was 2.2M cycles per launch before.
+__host__ __device__ constexpr int col_slot(int c) { return c ^ ((c >> 1) & 1) ^ (((c >> 2) & 1) << 1); }
+
 // B^T row k of this item's 4x4 window (channel pair): the two window rows a0, a1 of group
 // k read from the padded slot (off-board entries are the zero border) -- issued first,
-// combined once the MFMAs they hide behind are under way
+// combined once the MFMAs they hide behind are under way.  cols = the window's four column
+// slots (col_slot(2tx + b), 8 bits each)
 template <class G>
-__device__ __forceinline__ void read_rows(f32x2 (&d)[8], const char* slot, int rbase, int L) {
+__device__ __forceinline__ void read_rows(f32x2 (&d)[8], const char* slot, int rbase, int cols,
+                                          int L) {
   const int k = L >> 3;
   const char* r0 = slot + rbase + grp_a0(k) * G::IN_ROW;
   const char* r1 = slot + rbase + grp_a1(k) * G::IN_ROW;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    d[b] = *reinterpret_cast<const f32x2*>(r0 + b * 64);
-    d[4 + b] = *reinterpret_cast<const f32x2*>(r1 + b * 64);
+    const int co = ((cols >> (8 * b)) & 0xff) * 64;
+    d[b] = *reinterpret_cast<const f32x2*>(r0 + co);
+    d[4 + b] = *reinterpret_cast<const f32x2*>(r1 + co);
   }
 }
 
@@ -243,9 +256,10 @@ __device__ __forceinline__ void combine_rows(f32x2 (&rk)[4], const f32x2 (&d)[8]
 }
 
 template <class G>
-__device__ __forceinline__ void make_rows(f32x2 (&rk)[4], const char* slot, int rbase, int L) {
+__device__ __forceinline__ void make_rows(f32x2 (&rk)[4], const char* slot, int rbase, int cols,
+                                          int L) {
   f32x2 d[8];
-  read_rows<G>(d, slot, rbase, L);
+  read_rows<G>(d, slot, rbase, cols, L);
   combine_rows(rk, d, L);
 }
 
@@ -333,7 +347,7 @@ struct St {
   Frag<G> bf[G::RING], af[G::NRT];
   f32x16 acc[4][G::NRT];
   f32x16 Y[2][2][G::NRT];
-  int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], soff[G::TPT], aoff[G::NRT];
+  int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], cols[G::TPT], soff[G::TPT], aoff[G::NRT];
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
   int wlane, tid, b0, nb;
   unsigned lds_res;   // LDS byte address of this wave's first residual piece
@@ -446,7 +460,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
   // the next chunk's window rows (chunk L+2, stored just before the barrier)
 #pragma unroll
   for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.rbase[u], Ls);
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
 }
 
 template <class G>
@@ -547,7 +561,10 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   for (int u = 0; u < G::TPT; ++u) {
     const int T = (tid >> 3) + u * (G::THREADS / 8), p = tid & 7;
     const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
-    S.rbase[u] = bd * G::IN_BOARD + 2 * ty * G::IN_ROW + 2 * tx * 64 + p * 8;
+    S.rbase[u] = bd * G::IN_BOARD + 2 * ty * G::IN_ROW + p * 8;
+    S.cols[u] = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) S.cols[u] |= col_slot(2 * tx + b) << (8 * b);
     S.soff[u] = T * 32 + (((p >> 2) ^ ((T >> 3) & 1)) << 4) + (p & 3) * 4;
     S.vsc[u] = 1.0f;
     if constexpr (G::SCALED) {
@@ -562,11 +579,14 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   // channel quad e % 4 of the chunk
 #pragma unroll
   for (int j = 0; j < G::LD_PER_THREAD; ++j) {
-    const int e = j * G::THREADS + tid, P = e >> 2, q = e & 3;
+    // lanes 4i..4i+3 load position P; positions of a 4-aligned group are visited in the
+    // order 0, 2, 1, 3 so each 8-lane store group writes columns (c, c + 2) (col_slot)
+    const int e = j * G::THREADS + tid, P0 = e >> 2, q = e & 3;
+    const int P = (P0 & ~3) | ((P0 & 1) << 1) | ((P0 >> 1) & 1);
     const int bd = P >> 6, pos = P & 63;
     const int bs = bd < nb ? bd : nb - 1;
     S.goff[j] = ((b0 + bs) * 64 + pos) * C + 4 * q;
-    S.ldst[j] = bd * G::IN_BOARD + ((pos >> 3) + 1) * G::IN_ROW + ((pos & 7) + 1) * 64 + q * 16;
+    S.ldst[j] = bd * G::IN_BOARD + ((pos >> 3) + 1) * G::IN_ROW + col_slot((pos & 7) + 1) * 64 + q * 16;
   }
 
   // ---- prologue: zero both input slots (their borders stay zero), chunk 0 and 1 slices and
@@ -587,7 +607,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     if (G::IPD == 1) load_in<G>(S.ld[0], x, S.goff, 2);  // stored at the end of chunk 0
     lds_barrier();
 #pragma unroll
-    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], 0);
+    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], S.cols[u], 0);
   }
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u) {
@@ -602,7 +622,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   read_a<G>(S.af, S.lds, 0, S.aoff);
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], 1);
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], S.cols[u], 1);
   // epilogue constants: bias, and (FP16X2) the scale M carries, 2^(su + sv_board); removing
   // it is an exact power-of-two product
   Epi<G> E;
@@ -710,8 +730,9 @@ extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float*
   AZ_REQUIRE(mode != AZ_CONV_FP16X2 || (in_absmax && in_absmax != out_absmax), AZ_ERR_ARG,
              "az_conv3x3_wino4_gpu: FP16X2 needs in_absmax (distinct from out_absmax)");
   hipStream_t s = azc::as_stream(stream);
-  // AZ_W4_NRT (experiments): 1 = eight waves of one row tile, 2 = four waves of two
-  static const int nrt = getenv("AZ_W4_NRT") ? atoi(getenv("AZ_W4_NRT")) : 2;
+  // AZ_W4_NRT (experiments): 1 = eight waves of one row tile (default: two waves per SIMD,
+  // no AGPR traffic in the fold; bench 79.7 vs 73.5 games/s same-box), 2 = four waves of two
+  static const int nrt = getenv("AZ_W4_NRT") ? atoi(getenv("AZ_W4_NRT")) : 1;
 #define W4_GO(M, N) launch_wino4<W4<M, N>>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, s)
   if (mode == AZ_CONV_SPLIT3) return nrt == 1 ? W4_GO(AZ_CONV_SPLIT3, 1) : W4_GO(AZ_CONV_SPLIT3, 2);
   if (mode == AZ_CONV_FP16) return nrt == 1 ? W4_GO(AZ_CONV_FP16, 1) : W4_GO(AZ_CONV_FP16, 2);

@@ -12,7 +12,8 @@ import az_native as nat  # noqa: E402
 
 def main():
     name, mode_name, B, reps = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-    mode = {"split3": nat.AZ_CONV_SPLIT3, "fp16": nat.AZ_CONV_FP16}[mode_name]
+    mode = {"split3": nat.AZ_CONV_SPLIT3, "fp16": nat.AZ_CONV_FP16,
+            "fp16x2": nat.AZ_CONV_FP16X2}[mode_name]
     dev = torch.device("cuda")
     C = 128
     g = torch.Generator().manual_seed(0)
@@ -21,16 +22,25 @@ def main():
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
     planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
     direct = name == "az_conv3x3_mx_gpu"
-    wq = torch.empty((9 if direct else 16) * C * C * planes, dtype=torch.int16, device=dev)
+    nbytes = (9 * C * C * planes * 2 if direct else nat.lib.az_conv3x3_wino_prep_bytes(C, mode))
+    wq = torch.empty(nbytes // 2, dtype=torch.int16, device=dev)
     prep = nat.lib.az_conv3x3_mx_prep_gpu if direct else nat.lib.az_conv3x3_wino_prep_gpu
     nat.check(prep(nat.ptr(w9), nat.ptr(wq), C, mode, nat.stream_ptr()), "prep")
     x = torch.randn(B, C, 8, 8, device=dev).relu().contiguous(memory_format=torch.channels_last)
     r = torch.randn_like(x).relu().contiguous(memory_format=torch.channels_last)
     y = torch.empty_like(x)
     fn = getattr(nat.lib, name)
+    args = [nat.ptr(x), nat.ptr(wq), nat.ptr(bias), nat.ptr(r), nat.ptr(y), B, C, 1, mode]
+    amax = work = None
+    if "wino4" in name:
+        from Models import board_absmax
+        amax = board_absmax(x)
+        work = amax.clone()
+        args += [nat.ptr(work), None]
     for _ in range(reps):
-        nat.check(fn(nat.ptr(x), nat.ptr(wq), nat.ptr(bias), nat.ptr(r), nat.ptr(y), B, C, 1, mode,
-                     nat.stream_ptr()), name)
+        if work is not None:
+            work.copy_(amax)  # the kernel consumes (zeroes) its in_absmax
+        nat.check(fn(*args, nat.stream_ptr()), name)
     torch.cuda.synchronize()
     print("ok", name, mode_name, B, reps)
 

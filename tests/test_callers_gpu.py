@@ -1,0 +1,81 @@
+"""the interactive callers run unchanged on the drop-in MCTS.
+
+play_othello.py:39-94 (human vs MCTS) and play_mcts_vs_egaroucid.py:191-240 (MCTS vs an
+external engine) drive one `MCTS(env, {'c_puct', 'num_simulations'}, net,
+apply_symmetry=True)` through a whole game: `policy_improve_step(state, player, temp=0.0)`
+on the bot's turns, the opponent's move chosen outside MCTS, `mcts.make_move(a)` after
+EVERY ply (both sides, tree reuse), and `(mcts.root.value + 1) / 2 if mcts.root` read as
+the win probability.  Here the opponent is a seeded random legal mover (the human / the
+Egaroucid engine stand-in) and the net is the deterministic mock policy; the expected
+moves and root values come from the oracle's sequential restatement of the reference
+MCTS (oracle/mcts.py, pinned to reference-run goldens), with np.random seeded identically
+before every search (temp 0 breaks count ties with np.random.choice, MCTS_model.py:247).
+Bit-exact: every bot move, every root value and visit count."""
+import numpy as np
+import pytest
+
+from mock_policy import MockPolicy, mock_eval
+
+pytestmark = pytest.mark.gpu
+
+nat = pytest.importorskip("az_native")
+from MCTS_model import MCTS  # noqa: E402
+from envs.othello import OthelloGameNew  # noqa: E402
+from oracle import board as ob  # noqa: E402
+from oracle.mcts import SeqMCTS  # noqa: E402
+
+
+def _oracle_eval(own, opp, player):
+    st = ob.to_state(own, opp, player)
+    p, v = mock_eval((player * st).reshape(-1))
+    return p.astype(np.float32), float(v)
+
+
+def _play(bot_player, sims, seed):
+    env = OthelloGameNew(8)
+    args = {"c_puct": 3.0, "num_simulations": sims}  # play_othello.py:41's keys
+    mcts = MCTS(env, args, MockPolicy(), apply_symmetry=True)
+    ref = SeqMCTS(args["c_puct"], sims, _oracle_eval)
+    opp_rng = np.random.default_rng(seed)
+    game = ob.OracleGame()
+    state, ostate = env.get_initial_state(), game.get_initial_state()
+    player, plies, bot_moves = 1, 0, 0
+    while True:
+        assert (np.asarray(state) == np.asarray(ostate)).all()
+        if player == bot_player:
+            np.random.seed(seed * 1000 + plies)
+            probs = mcts.policy_improve_step(state, player, temp=0.0)
+            np.random.seed(seed * 1000 + plies)
+            own, opp = ob.to_bitboards(ostate, player)
+            rprobs = ref.search(own, opp, player, 0.0)
+            action = int(np.argmax(probs))
+            assert action == int(np.argmax(rprobs)), plies
+            got = np.array([c.visit_count if c else 0 for c in
+                            (mcts.root.children.get(a) for a in range(65))])
+            assert (got == ref.root_counts()).all(), plies
+            bot_moves += 1
+        else:
+            valid = np.flatnonzero(env.get_valid_moves(state, player))
+            action = int(opp_rng.choice(valid))
+        mcts.make_move(action)
+        if ref.root >= 0:
+            ref.make_move(action)
+        # play_othello.py:71
+        win_prob = (mcts.root.value + 1) / 2 if mcts.root else 0.0
+        exp = (ref.value(0) + 1) / 2 if ref.root >= 0 else 0.0
+        assert win_prob == exp, plies
+        state = env.get_next_state(state, action, player)
+        ostate = game.get_next_state(ostate, action, player)
+        value, done = env.get_value_and_terminated(state, action, player)
+        ovalue, odone = game.get_value_and_terminated(ostate, action, player)
+        assert (value, done) == (ovalue, odone)
+        plies += 1
+        if done:
+            return plies, bot_moves
+        player = env.get_opponent(player)
+
+
+@pytest.mark.parametrize("bot_player,seed", [(1, 1), (-1, 2)])
+def test_interactive_caller_loop_matches_reference(bot_player, seed):
+    plies, bot_moves = _play(bot_player, sims=24, seed=seed)
+    assert plies >= 30 and bot_moves >= 15
