@@ -7,7 +7,7 @@ from collections import defaultdict
 
 for prefix in sys.argv[1:]:
     vals = defaultdict(list)
-    for f in sorted(glob.glob(prefix + "_*/pmc_counter_collection.csv")):
+    for f in sorted(glob.glob(prefix + "_[0-9]*/pmc_counter_collection.csv")):
         rows = list(csv.DictReader(open(f)))
         per = defaultdict(lambda: defaultdict(float))
         for r in rows:
