@@ -101,8 +101,8 @@ def parse():
                          "(c5's fp16 inference)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=8,
-                    help="simulation steps captured per HIP graph (1 under rocprofv3: its "
-                         "kernel tracer crashes on multi-step captures)")
+                    help="simulation steps captured per HIP graph (rocprofv3's kernel tracer "
+                         "records 8-step graphs completely: DESIGN.md section 5)")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=8,
