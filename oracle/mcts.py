@@ -14,6 +14,15 @@ Every float operation reproduces the reference's NumPy-2 (NEP 50) promotion expl
   * backup alternates sign from the leaf to the root                     (:160-169)
   * pi from child visit counts                                           (:244-274)
 
+leaves_per_step = K > 1 restates the reference's threaded search (args['num_threads'] = K,
+:196-197, :237-242, :372-395) in the one fixed interleaving the engine implements and
+tests/golden/make_vl_goldens.py forces on the reference: simulations start one at a time;
+each adds a virtual loss to every node it passes (:115-118) -- Node.value = (W + VV) / (N + VV),
+PUCT counts the parent's and children's virtual visits (:110-139); a terminal one backs up
+at once; one reaching an unexpanded leaf waits (its virtual loss stays) until K wait or the
+simulations are all started; the waiting ones then finish in start order (expand once per
+distinct leaf, back up each one's value).
+
 RNG draws go through an adapter so a test can either replay the reference's global
 np.random stream call-for-call (NumpyRng) or inject recorded draws (LogRng).
 """
@@ -67,18 +76,20 @@ class LogRng:
         return int(cdf.searchsorted(u, side="right"))
 
 
-def ucb_scores(prior, n_child, w_child, n_parent, c_puct):
-    """PUCT of every child (MCTS_model.py:129-139) with the parent's +1 virtual visit."""
+def ucb_scores(prior, n_child, w_child, n_parent, c_puct, vv_parent=1, vv_child=None):
+    """PUCT of every child (MCTS_model.py:129-139) with the parent's virtual visits (its
+    own +1 during the descent, plus those of waiting simulations) and the children's."""
     out = []
-    sq = math.sqrt(n_parent + 1 + 1e-8)
-    for p, n, w in zip(prior, n_child, w_child):
-        q = -(0.0 if n == 0 else w / n)
+    sq = math.sqrt(n_parent + vv_parent + 1e-8)
+    vv_child = vv_child or [0] * len(prior)
+    for p, n, w, vv in zip(prior, n_child, w_child, vv_child):
+        q = -(0.0 if n + vv == 0 else (w + float(vv)) / (n + vv))
         if isinstance(p, np.float64):
-            u = c_puct * float(p) * sq / (1 + n)
+            u = c_puct * float(p) * sq / (1 + n + vv)
             out.append(q + u)
         else:
             u = np.float32(np.float32(np.float32(np.float32(c_puct) * p) * np.float32(sq))
-                           / np.float32(1 + n))
+                           / np.float32(1 + n + vv))
             out.append(np.float32(np.float32(q) + u))
     return out
 
@@ -87,8 +98,9 @@ class SeqMCTS:
     """Flat-array tree; node 0 is the root after every re-root."""
 
     def __init__(self, c_puct, num_simulations, evaluate=None, dirichlet_alpha=0.03,
-                 dirichlet_epsilon=0.0, rng=None):
+                 dirichlet_epsilon=0.0, rng=None, leaves_per_step=1):
         self.c_puct = c_puct
+        self.K = max(1, int(leaves_per_step))
         self.sims = num_simulations
         self.evaluate = evaluate  # (own, opp, player) -> (priors f32[65], value float)
         self.alpha = dirichlet_alpha
@@ -162,6 +174,9 @@ class SeqMCTS:
                 return 1 if d > 0 else (-1 if d < 0 else 0)
 
     def _expand(self, i):
+        self._backup(i, self._expand_only(i))
+
+    def _expand_only(self, i):
         if self.evaluate is None:
             priors = np.ones(65, np.float32)
             v = self._rollout(self.own[i], self.opp[i])
@@ -182,7 +197,7 @@ class SeqMCTS:
             own, opp = ob.make_move(self.own[i], self.opp[i], a)
             c = self._new(own, opp, -self.player[i], i, a, priors[a], False)
             self.kids[i].append(c)
-        self._backup(i, v)
+        return v
 
     def _select(self, i):
         kids = self.kids[i]
@@ -205,6 +220,42 @@ class SeqMCTS:
                 return
             i = self._select(i)
 
+    def _select_vl(self, i, vv):
+        kids = self.kids[i]
+        sc = ucb_scores([self.prior[k] for k in kids], [self.N[k] for k in kids],
+                        [self.W[k] for k in kids], self.N[i], self.c_puct,
+                        1 + vv.get(i, 0), [vv.get(k, 0) for k in kids])
+        best = 0
+        for j in range(1, len(kids)):
+            if sc[j] > sc[best]:
+                best = j
+        return kids[best]
+
+    def simulate_batch(self, remaining):
+        """One engine step of the K-leaf search: returns the simulations it completed."""
+        done, pending, vv = 0, [], {}
+        while done + len(pending) < remaining and len(pending) < self.K:
+            i, path = self.root, []
+            while True:
+                path.append(i)
+                if self.term[i]:
+                    self._backup(i, self.tval[i])
+                    done += 1
+                    break
+                if not self.kids[i]:
+                    pending.append(i)
+                    for n in path:
+                        vv[n] = vv.get(n, 0) + 1
+                    break
+                i = self._select_vl(i, vv)
+        values = {}
+        for leaf in pending:
+            if leaf not in values:
+                values[leaf] = self._expand_only(leaf)
+            self._backup(leaf, values[leaf])
+            done += 1
+        return done
+
     def search(self, own, opp, player, temp=1.0):
         """policy_improve_step (MCTS_model.py:217-274)."""
         if self.root < 0:
@@ -214,8 +265,13 @@ class SeqMCTS:
             assert self.player[self.root] == player
         if not self.kids[self.root]:
             self._expand(self.root)
-        for _ in range(self.sims):
-            self.simulate()
+        if self.K == 1:
+            for _ in range(self.sims):
+                self.simulate()
+        else:
+            done = 0
+            while done < self.sims:
+                done += self.simulate_batch(self.sims - done)
         counts = np.zeros(65, np.float32)
         for k in self.kids[self.root]:
             counts[self.action[k]] = self.N[k]

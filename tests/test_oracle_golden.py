@@ -122,6 +122,60 @@ def test_mcts_cases_match_reference(case):
     replay_case(d, case)
 
 
+def replay_vl_case(d, c):
+    """One multi-leaf (virtual-loss) golden case: the reference's threaded search forced
+    into the engine's interleaving (tests/golden/make_vl_goldens.py), on the oracle."""
+    rows = np.nonzero(d["log_case"] == c)[0]
+    nlo, nhi = d["noise_offsets"][c], d["noise_offsets"][c + 1]
+    n = nhi - nlo
+    rng = LogRng(np.zeros(n, np.int32), np.arange(n, dtype=np.float64), np.zeros(n, np.int64),
+                 d["noise"][nlo:nhi])
+    r0 = rows[0]
+    mp = MockPolicy()
+
+    def evaluate(own, opp, player):
+        return mp.inference(ob.to_state(own, opp, player), player)
+
+    m = SeqMCTS(float(d["c_puct"][r0]), int(d["sims"][r0]), evaluate, dirichlet_alpha=1.0,
+                dirichlet_epsilon=float(d["eps"][r0]), rng=rng, leaves_per_step=int(d["k"][r0]))
+    for r in rows:
+        own, opp = own_opp(d["pos"][r], d["neg"][r], d["player"][r])
+        probs = m.search(int(own), int(opp), int(d["player"][r]), 1.0)
+        assert (m.root_counts() == d["counts"][r]).all(), f"case {c} move {d['moves'][r]}"
+        assert m.value(m.root) == d["root_value"][r]
+        assert (probs.astype(np.float32) == d["probs"][r]).all()
+        assert m.N[m.root] == d["root_n"][r]
+        if r != rows[-1]:
+            m.make_move(int(np.argmax(d["counts"][r])))
+    assert rng.i == len(rng.kinds)
+
+
+@pytest.mark.parametrize("case", range(28))
+def test_mcts_virtual_loss_cases_match_reference(case):
+    d = load_golden("mcts_vl_cases.npz")
+    assert int(d["n_cases"]) == 28
+    replay_vl_case(d, case)
+
+
+def test_virtual_loss_cases_differ_from_single_leaf():
+    """The K-leaf goldens are not the num_threads=1 search (the virtual loss matters)."""
+    d = load_golden("mcts_vl_cases.npz")
+    mp = MockPolicy()
+
+    def evaluate(own, opp, player):
+        return mp.inference(ob.to_state(own, opp, player), player)
+
+    differ = 0
+    for r in np.nonzero(d["moves"] == 0)[0]:
+        if d["eps"][r] > 0:
+            continue
+        m = SeqMCTS(float(d["c_puct"][r]), int(d["sims"][r]), evaluate)
+        own, opp = own_opp(d["pos"][r], d["neg"][r], d["player"][r])
+        m.search(int(own), int(opp), int(d["player"][r]), 1.0)
+        differ += int((m.root_counts() != d["counts"][r]).any())
+    assert differ >= 3
+
+
 def _selfplay_args(sims):
     return {"c_puct": 2.0, "num_simulations": sims, "dirichlet_alpha": 1.0,
             "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
