@@ -57,6 +57,7 @@ class AzConfig(ctypes.Structure):
         ("inj_uniform_slots", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("stream_id", ctypes.c_uint64),
+        ("leaves_per_step", ctypes.c_int32),
     ]
 
 

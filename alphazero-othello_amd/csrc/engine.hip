@@ -41,6 +41,7 @@ constexpr int kWave = 64;
 constexpr int kSelBlock = 256;  // 4 slots (waves) per workgroup in select / expand
 constexpr int kMoveBlock = 256;
 constexpr int kMaxPath = 64;     // one wave lane per path depth for the parallel backup
+constexpr int kMaxLeaves = 8;    // leaves_per_step limit (virtual-loss descents per step)
 
 enum : uint8_t { kExpanded = 1, kTerminal = 2, kChildF64 = 4 };
 enum : int32_t { kIdle = AZ_GAME_IDLE, kActive = AZ_GAME_ACTIVE, kFinished = AZ_GAME_FINISHED,
@@ -68,16 +69,16 @@ struct Games {
   int32_t* n_nodes;
   int32_t* sims_done;
   int32_t* sims_target;
-  int32_t* leaf;       // leaf awaiting evaluation, -1 none
-  int32_t* path;       // [G, kMaxPath] root..leaf node indices of the pending leaf
-  int32_t* path_len;   // entries in `path`; 0 => deeper than kMaxPath, walk parents
+  int32_t* leaf;       // [G, K] leaves awaiting evaluation in descent order, -1 ends the list
+  int32_t* path;       // [G, K, kMaxPath] root..leaf node indices of each pending leaf
+  int32_t* path_len;   // [G, K] entries in `path`; 0 => deeper than kMaxPath, walk parents
   int32_t* ply;
   int32_t* root_player;
   int32_t* winner;
   int32_t* overflow;
   int32_t* start_step; // slot becomes active at this engine step (stagger)
   uint32_t* rng_event; // per-slot RNG event counter
-  uint8_t* sym;        // D4 transform of the pending leaf
+  uint8_t* sym;        // [G, K] D4 transform of each pending leaf
   int32_t* noise_cur;  // injected-stream cursors
   int32_t* u_cur;
   // trajectory [G, T]
@@ -123,6 +124,7 @@ struct Params {
   const double* inj_u;      // [G, NU]
   int32_t G, C, T, NS, NU;
   int32_t sims;
+  int32_t K;  // leaves per slot per step (virtual loss, MCTS_model.py num_threads)
   int32_t n_explore;
   int32_t eval_mode, rng_mode, d4, auto_play, refill;
   double c_puct, alpha, eps, temp, lambd;
@@ -213,17 +215,17 @@ __device__ void backup_path(const Params& p, int g, int half, int path_node, int
 
 // Pack the canonical NN input player*state (Models.py:16): own stones +1, opponent -1,
 // optionally through D4 transform `sym` (random_symmetry, MCTS_model.py:15-28).
-__device__ void emit_leaf(const Params& p, float* nn_in, int g, uint64_t own, uint64_t opp,
+__device__ void emit_leaf(const Params& p, float* nn_in, int64_t row, uint64_t own, uint64_t opp,
                           int sym) {
   const int lane = lane_id();
   const float v = ((own >> lane) & 1) ? 1.0f : (((opp >> lane) & 1) ? -1.0f : 0.0f);
   const int dst = sym ? azb::d4_square(lane, sym) : lane;
-  nn_in[(int64_t)g * 64 + dst] = v;
+  nn_in[row * 64 + dst] = v;
 }
 
-__device__ void emit_none(float* nn_in, int32_t* leaf_o, int g) {
-  nn_in[(int64_t)g * 64 + lane_id()] = 0.0f;
-  if (lane_id() == 0 && leaf_o) leaf_o[g] = -1;
+__device__ void emit_none(float* nn_in, int32_t* leaf_o, int64_t row) {
+  nn_in[row * 64 + lane_id()] = 0.0f;
+  if (lane_id() == 0 && leaf_o) leaf_o[row] = -1;
 }
 
 // What the descent needs of a node, loaded together with its siblings' PUCT inputs so that
@@ -316,11 +318,93 @@ __device__ void push_ready(const Params& p, int g) {
 // ---------------------------------------------------------------------------------
 // k_select
 
+// Virtual visits of the descents waiting for evaluation in this step (leaves_per_step > 1,
+// the reference's num_threads workers, MCTS_model.py:115-118, :196-197): lane d of path[j]
+// holds waiting descent j's node at depth d (-1 past its leaf).  A node at depth d can only
+// sit at depth d of a path, so its virtual visits are the waiting paths holding it there.
+template <int KMAX>
+struct Waiting {
+  int path[KMAX];
+  int n;
+};
+
+template <int KMAX>
+__device__ __forceinline__ int virtual_visits(const Waiting<KMAX>& w, int depth, int node) {
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j < w.n) c += __shfl(w.path[j], depth, kWave) == node ? 1 : 0;
+  return c;
+}
+
+// select_child_rec with virtual loss (Node.value = (W + VV) / (N + VV), the parent's own
+// and the waiting descents' visits in the sqrt term, 1 + N + VV below it: MCTS_model.py:
+// 110-114, :129-139).  With no waiting descent this is select_child_rec's arithmetic.
+template <int KMAX>
+__device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeRec& par,
+                                   int depth, const Waiting<KMAX>& w) {
+  const int lane = lane_id();
+  const int nc = rec_nchild(par);
+  const int fc = par.first;
+  const bool f64 = (rec_flags(par) & kChildF64) != 0;
+  const int vvp = 1 + virtual_visits(w, depth, par.node);
+  const double sq = sqrt((double)(par.visits + vvp) + 1e-8);
+  const int vvc = depth + 1 < kMaxPath ? virtual_visits(w, depth + 1, fc + lane) : 0;
+  double score = -INFINITY;
+  int idx = 0x7fffffff;
+  NodeRec mine{0, 0, 0, 0, 0ull, 0ull};
+  if (lane < nc) {
+    const int64_t c = nidx(p, half, g, fc + lane);
+    const int n = p.a.N[c];
+    const double wv = p.a.W[c];
+    const double pr = p.a.P[c];
+    mine.first = p.a.first[c];
+    mine.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
+    mine.visits = n;
+    mine.own = p.a.own[c];
+    mine.opp = p.a.opp[c];
+    const int nv = n + vvc;
+    const double q = -(nv == 0 ? 0.0 : (wv + (double)vvc) / (double)nv);
+    if (f64) {
+      const double u = p.c_puct * pr * sq / (double)(1 + nv);
+      score = q + u;
+    } else {
+      const float u = (((float)p.c_puct * (float)pr) * (float)sq) / (float)(1 + nv);
+      score = (double)((float)q + u);
+    }
+    idx = lane;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double os = __shfl_xor(score, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    if (os > score || (os == score && oi < idx)) {
+      score = os;
+      idx = oi;
+    }
+  }
+  NodeRec r;
+  r.node = fc + idx;
+  r.first = __shfl(mine.first, idx, kWave);
+  r.visits = __shfl(mine.visits, idx, kWave);
+  r.meta = __shfl(mine.meta, idx, kWave);
+  r.own = __shfl(mine.own, idx, kWave);
+  r.opp = __shfl(mine.opp, idx, kWave);
+  return r;
+}
+
+// KMAX = 1: one leaf per slot per step (num_threads = 1).  KMAX > 1: up to K = p.K leaves,
+// descents run one after another, each seeing the earlier ones' virtual loss; terminal
+// descents back up at once, the others wait for the batched evaluation in rows
+// nn_in[g*K + j] (the interleaving tests/golden/make_vl_goldens.py forces on the reference).
+template <int KMAX>
 __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restrict__ nn_in,
                                                       int32_t* __restrict__ leaf_o,
                                                       int max_descents) {
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
+  const int K = KMAX == 1 ? 1 : p.K;
+  const int64_t row0 = (int64_t)g * K;
   const int lane = lane_id();
   // every per-slot word in one round trip
   const int status = p.g.status[g];
@@ -330,24 +414,56 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   int sims_done = p.g.sims_done[g];
   const int target = p.g.sims_target[g];
   if (status != kActive || (long long)step < (long long)start_step) {
-    emit_none(nn_in, leaf_o, g);
+    for (int j = 0; j < K; ++j) emit_none(nn_in, leaf_o, row0 + j);
     return;
   }
-  int leaf = -1;
+  Waiting<KMAX> w;
+  w.n = 0;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) w.path[j] = -1;
+  bool deep = false;  // a waiting path past kMaxPath: its virtual loss could not be tracked
   int depth = 0;      // depth of the current node
   int path_node = 0;  // lane d: node at depth d of the current descent
   NodeRec cur = load_rec(p, g, half, 0);
+  // the leaf in `cur` waits for evaluation as row g*K + w.n
+  auto wait_leaf = [&]() {
+    const int j = w.n;
+    const int64_t row = row0 + j;
+    int sym = 0;
+    if (p.d4) {
+      const uint32_t ev = p.g.rng_event[g];
+      sym = (int)(azr::uniform1(p.seed, (uint32_t)g, ev, 0x5000u, p.stream_id) * 8.0) & 7;
+      if (lane == 0) {
+        p.g.rng_event[g] = ev + 1;
+        p.g.sym[row] = (uint8_t)sym;
+      }
+    }
+    emit_leaf(p, nn_in, row, cur.own, cur.opp, sym);
+    const bool held = depth < kMaxPath && lane <= depth;
+    if (held) p.g.path[row * kMaxPath + lane] = path_node;
+    if (lane == 0) {
+      p.g.path_len[row] = depth < kMaxPath ? depth + 1 : 0;
+      p.g.leaf[row] = cur.node;
+      if (leaf_o) leaf_o[row] = cur.node;
+    }
+    if constexpr (KMAX > 1) {
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (jj == j) w.path[jj] = held ? path_node : -1;
+      deep = deep || depth >= kMaxPath;
+    }
+    w.n = j + 1;
+  };
   if (!(rec_flags(cur) & kExpanded)) {
-    leaf = 0;  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
+    wait_leaf();  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
   } else {
     int guard = 0;
-    while (sims_done < target && guard < max_descents) {
+    while (sims_done + w.n < target && w.n < K && guard < max_descents) {
       if (guard > 0) cur = load_rec(p, g, half, 0);  // the last backup changed the root's N
       ++guard;
       depth = 0;
       path_node = 0;
-      bool done = false;
-      while (!done) {
+      while (true) {
         const uint8_t f = rec_flags(cur);
         if (f & kTerminal) {  // MCTS_model.py:381-384
           const double tv = (double)rec_tval(cur);
@@ -359,38 +475,25 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
           // the N/W stores must be visible to the wave's next PUCT loads
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
           ++sims_done;
-          done = true;
-        } else if (!(f & kExpanded)) {  // MCTS_model.py:386-389
-          leaf = cur.node;
-          done = true;
-        } else {
-          cur = select_child_rec(p, g, half, cur);
-          ++depth;
-          if (lane == depth) path_node = cur.node;
+          break;
         }
+        if (!(f & kExpanded)) {  // MCTS_model.py:386-389
+          wait_leaf();
+          break;
+        }
+        if constexpr (KMAX == 1) {
+          cur = select_child_rec(p, g, half, cur);
+        } else {
+          cur = select_child_vl<KMAX>(p, g, half, cur, depth, w);
+        }
+        ++depth;
+        if (lane == depth) path_node = cur.node;
       }
-      if (leaf >= 0) break;
     }
   }
-  if (leaf >= 0) {
-    int sym = 0;
-    if (p.d4) {
-      const uint32_t ev = p.g.rng_event[g];
-      sym = (int)(azr::uniform1(p.seed, (uint32_t)g, ev, 0x5000u, p.stream_id) * 8.0) & 7;
-      if (lane == 0) {
-        p.g.rng_event[g] = ev + 1;
-        p.g.sym[g] = (uint8_t)sym;
-      }
-    }
-    emit_leaf(p, nn_in, g, cur.own, cur.opp, sym);  // cur = the leaf's record
-    if (depth < kMaxPath && lane <= depth) p.g.path[(int64_t)g * kMaxPath + lane] = path_node;
-    if (lane == 0) {
-      p.g.path_len[g] = depth < kMaxPath ? depth + 1 : 0;
-      p.g.leaf[g] = leaf;
-      if (leaf_o) leaf_o[g] = leaf;
-    }
-  } else {
-    emit_none(nn_in, leaf_o, g);
+  for (int j = w.n; j < K; ++j) {
+    emit_none(nn_in, leaf_o, row0 + j);
+    if (KMAX > 1 && lane == 0) p.g.leaf[row0 + j] = -1;
   }
   if (lane == 0) {
     const int prev = p.g.sims_done[g];
@@ -398,9 +501,13 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       atomicAdd(&p.ctr->sims, (unsigned long long)(sims_done - prev));
       p.g.sims_done[g] = sims_done;
     }
-    if (leaf < 0 && sims_done >= target) {
+    if (w.n == 0 && sims_done >= target) {
       if (p.auto_play) push_ready(p, g);
       else p.g.status[g] = kSearchDone;
+    }
+    if (deep) {
+      p.g.overflow[g] += 1;
+      atomicAdd(&p.ctr->overflow, 1ull);
     }
   }
 }
@@ -436,22 +543,20 @@ __device__ double rollout(const Params& p, int g, uint64_t own, uint64_t opp) {
   return 0.0;
 }
 
-__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
-                                                      const float* __restrict__ values) {
-  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
-  if (g >= p.G) return;
+// One waiting leaf (row `row` of the evaluation batch): evaluate, expand and back up
+// (MCTS_model.py:325-360).  `repeat`: an earlier descent of this step waits on the same
+// leaf -- it is expanded already and this descent only backs up that descent's value `v_in`
+// (two reference workers on one leaf both expand it, the second with identical fresh
+// children, and both back up).  Returns the value backed up.
+__device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t row, int leaf,
+                                     int plen, int pn, const float* __restrict__ priors,
+                                     const float* __restrict__ values, bool repeat,
+                                     double v_in) {
   const int lane = lane_id();
-  // the slot's state and its recorded path in one round trip (the path entries are valid
-  // memory whatever their contents; they are used only when a leaf is pending)
-  const int leaf = p.g.leaf[g];
-  const int half = p.g.half[g];
-  const int plen = p.g.path_len[g];
-  const int pn = p.g.path[(int64_t)g * kMaxPath + lane];
-  if (leaf < 0) return;
   const int64_t k = nidx(p, half, g, leaf);
   const uint64_t own = p.a.own[k], opp = p.a.opp[k], lg = p.a.legal[k];
   const bool is_root = leaf == 0;
-  // the path's N / W with the leaf's record (this kernel writes neither before the backup)
+  // the path's N / W with the leaf's record (nothing here writes them before the backup)
   const bool on_path = plen > 0 && lane < plen;
   int path_n = 0;
   double path_w = 0.0;
@@ -460,120 +565,121 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
     path_n = p.a.N[pk];
     path_w = p.a.W[pk];
   }
-
-  // ---- priors and value (MCTS_model.py:332-337)
-  float pr, pr64;
-  double v;
-  if (p.eval_mode == AZ_EVAL_ROLLOUT) {
-    pr = 1.0f;
-    pr64 = 1.0f;
-    double vv = 0.0;
-    if (lane == 0) vv = rollout(p, g, own, opp);
-    v = shfl(vv, 0);
-  } else {
-    const float* row = priors + (int64_t)g * 65;
-    const int sym = p.d4 ? p.g.sym[g] : 0;
-    // unsymmetrise_pi (MCTS_model.py:31-43): the net saw the board through `sym`
-    pr = row[sym ? azb::d4_square(lane, sym) : lane];
-    pr64 = row[64];
-    v = (double)values[g];
-  }
-  const bool valid = lg ? ((lg >> lane) & 1) != 0 : false;
-  const bool valid64 = lg == 0;
-
-  // ---- noise, mask, renormalise (MCTS_model.py:340-349)
-  const bool noise = is_root && p.eps > 0.0;
-  double P, P64;
-  if (noise) {
-    double n, n64;
-    if (p.rng_mode == AZ_RNG_INJECTED) {
-      const int cur = p.g.noise_cur[g];
-      const double* src = p.inj_noise + ((int64_t)g * p.NS + (cur < p.NS ? cur : p.NS - 1)) * 65;
-      n = src[lane];
-      n64 = src[64];
-      if (lane == 0) p.g.noise_cur[g] = cur + 1;
+  double v = v_in;
+  if (!repeat) {
+    // ---- priors and value (MCTS_model.py:332-337)
+    float pr, pr64;
+    if (p.eval_mode == AZ_EVAL_ROLLOUT) {
+      pr = 1.0f;
+      pr64 = 1.0f;
+      double vv = 0.0;
+      if (lane == 0) vv = rollout(p, g, own, opp);
+      v = shfl(vv, 0);
     } else {
-      const uint32_t ev = p.g.rng_event[g];
-      const double ga = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, (uint32_t)lane, p.stream_id);
-      const double ga64 = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, 64u, p.stream_id);
-      double s = ga;
+      const float* prow = priors + row * 65;
+      const int sym = p.d4 ? p.g.sym[row] : 0;
+      // unsymmetrise_pi (MCTS_model.py:31-43): the net saw the board through `sym`
+      pr = prow[sym ? azb::d4_square(lane, sym) : lane];
+      pr64 = prow[64];
+      v = (double)values[row];
+    }
+    const bool valid = lg ? ((lg >> lane) & 1) != 0 : false;
+    const bool valid64 = lg == 0;
+
+    // ---- noise, mask, renormalise (MCTS_model.py:340-349)
+    const bool noise = is_root && p.eps > 0.0;
+    double P, P64;
+    if (noise) {
+      double n, n64;
+      if (p.rng_mode == AZ_RNG_INJECTED) {
+        const int cur = p.g.noise_cur[g];
+        const double* src = p.inj_noise + ((int64_t)g * p.NS + (cur < p.NS ? cur : p.NS - 1)) * 65;
+        n = src[lane];
+        n64 = src[64];
+        if (lane == 0) p.g.noise_cur[g] = cur + 1;
+      } else {
+        const uint32_t ev = p.g.rng_event[g];
+        const double ga = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, (uint32_t)lane, p.stream_id);
+        const double ga64 = azr::gamma_draw(p.alpha, p.seed, (uint32_t)g, ev, 64u, p.stream_id);
+        double s = ga;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
-      s += ga64;
-      n = ga / s;
-      n64 = ga64 / s;
-      if (lane == 0) p.g.rng_event[g] = ev + 1;
-    }
-    // (1 - eps) * priors is float32 (Python float x float32 array); + eps * noise is float64
-    const float keep = (float)(1.0 - p.eps);
-    P = (double)(keep * pr) + p.eps * n;
-    P64 = (double)(keep * pr64) + p.eps * n64;
-    P = valid ? P : 0.0 * P;  // priors *= valid_mask
-    P64 = valid64 ? P64 : 0.0 * P64;
-    const double tot = np_sum65<double>(P, P64);
-    if (tot > 1e-12) {
-      P = P / tot;
-      P64 = P64 / tot;
-    }
-  } else {
-    float q = valid ? pr : 0.0f * pr;
-    float q64 = valid64 ? pr64 : 0.0f * pr64;
-    const float tot = np_sum65<float>(q, q64);
-    if (tot > (float)1e-12) {
-      q = q / tot;
-      q64 = q64 / tot;
-    }
-    P = (double)q;
-    P64 = (double)q64;
-  }
-
-  // ---- eager expansion of every legal child (MCTS_model.py:352-357, :146-158)
-  const int nc = lg ? azb::popc(lg) : 1;
-  int fc = 0;
-  if (lane == 0) {
-    fc = p.g.n_nodes[g];
-    if (fc + nc <= p.C) {
-      p.g.n_nodes[g] = fc + nc;
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+        s += ga64;
+        n = ga / s;
+        n64 = ga64 / s;
+        if (lane == 0) p.g.rng_event[g] = ev + 1;
+      }
+      // (1 - eps) * priors is float32 (Python float x float32 array); + eps * noise is float64
+      const float keep = (float)(1.0 - p.eps);
+      P = (double)(keep * pr) + p.eps * n;
+      P64 = (double)(keep * pr64) + p.eps * n64;
+      P = valid ? P : 0.0 * P;  // priors *= valid_mask
+      P64 = valid64 ? P64 : 0.0 * P64;
+      const double tot = np_sum65<double>(P, P64);
+      if (tot > 1e-12) {
+        P = P / tot;
+        P64 = P64 / tot;
+      }
     } else {
-      fc = -1;
-      p.g.overflow[g] += 1;
-      atomicAdd(&p.ctr->overflow, 1ull);
+      float q = valid ? pr : 0.0f * pr;
+      float q64 = valid64 ? pr64 : 0.0f * pr64;
+      const float tot = np_sum65<float>(q, q64);
+      if (tot > (float)1e-12) {
+        q = q / tot;
+        q64 = q64 / tot;
+      }
+      P = (double)q;
+      P64 = (double)q64;
     }
-  }
-  fc = shfl(fc, 0);
-  if (fc >= 0) {
-    const bool mine = lg ? valid : (lane == 0);
-    const int a = lg ? lane : azb::kPass;
-    uint64_t co = 0, cp = 0, clg = 0;
-    if (mine) {
-      azb::play(own, opp, a, lg ? azb::flips(own, opp, a) : 0ull, &co, &cp);
-      clg = azb::legal(co, cp);
-    }
-    // terminal check of every child, wave-cooperative for the rare real passes
-    int tf = azb::terminal_flags_wave(co, cp, clg, mine);
-    tf = azb::finish_terminal_wave(tf, co, cp);
-    if (mine) {
-      const int ci = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
-      const bool term = (tf & azb::kFlagTerminal) != 0;
-      const int d = azb::popc(co) - azb::popc(cp);
-      const int64_t c = nidx(p, half, g, fc + ci);
-      p.a.own[c] = co;
-      p.a.opp[c] = cp;
-      p.a.legal[c] = clg;
-      p.a.N[c] = 0;
-      p.a.W[c] = 0.0;
-      p.a.P[c] = lg ? P : P64;
-      p.a.parent[c] = leaf;
-      p.a.first[c] = -1;
-      p.a.nchild[c] = 0;
-      p.a.action[c] = (uint8_t)a;
-      p.a.flags[c] = term ? kTerminal : 0;
-      p.a.tval[c] = (int8_t)(term ? (d > 0 ? 1 : (d < 0 ? -1 : 0)) : 0);
-    }
+
+    // ---- eager expansion of every legal child (MCTS_model.py:352-357, :146-158)
+    const int nc = lg ? azb::popc(lg) : 1;
+    int fc = 0;
     if (lane == 0) {
-      p.a.first[k] = fc;
-      p.a.nchild[k] = (uint8_t)nc;
-      p.a.flags[k] = p.a.flags[k] | kExpanded | (noise ? kChildF64 : 0);
+      fc = p.g.n_nodes[g];
+      if (fc + nc <= p.C) {
+        p.g.n_nodes[g] = fc + nc;
+      } else {
+        fc = -1;
+        p.g.overflow[g] += 1;
+        atomicAdd(&p.ctr->overflow, 1ull);
+      }
+    }
+    fc = shfl(fc, 0);
+    if (fc >= 0) {
+      const bool mine = lg ? valid : (lane == 0);
+      const int a = lg ? lane : azb::kPass;
+      uint64_t co = 0, cp = 0, clg = 0;
+      if (mine) {
+        azb::play(own, opp, a, lg ? azb::flips(own, opp, a) : 0ull, &co, &cp);
+        clg = azb::legal(co, cp);
+      }
+      // terminal check of every child, wave-cooperative for the rare real passes
+      int tf = azb::terminal_flags_wave(co, cp, clg, mine);
+      tf = azb::finish_terminal_wave(tf, co, cp);
+      if (mine) {
+        const int ci = lg ? azb::popc(lg & ((1ull << lane) - 1ull)) : 0;
+        const bool term = (tf & azb::kFlagTerminal) != 0;
+        const int d = azb::popc(co) - azb::popc(cp);
+        const int64_t c = nidx(p, half, g, fc + ci);
+        p.a.own[c] = co;
+        p.a.opp[c] = cp;
+        p.a.legal[c] = clg;
+        p.a.N[c] = 0;
+        p.a.W[c] = 0.0;
+        p.a.P[c] = lg ? P : P64;
+        p.a.parent[c] = leaf;
+        p.a.first[c] = -1;
+        p.a.nchild[c] = 0;
+        p.a.action[c] = (uint8_t)a;
+        p.a.flags[c] = term ? kTerminal : 0;
+        p.a.tval[c] = (int8_t)(term ? (d > 0 ? 1 : (d < 0 ? -1 : 0)) : 0);
+      }
+      if (lane == 0) {
+        p.a.first[k] = fc;
+        p.a.nchild[k] = (uint8_t)nc;
+        p.a.flags[k] = p.a.flags[k] | kExpanded | (noise ? kChildF64 : 0);
+      }
     }
   }
   // backup (MCTS_model.py:360) along the path k_select recorded (backup_path's update on
@@ -585,13 +691,67 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
   } else if (plen == 0 && lane == 0) {
     backup(p, g, half, leaf, v);
   }
+  return v;
+}
+
+// One wavefront per slot: the slot's waiting leaves in descent order (rows g*K .. g*K+K-1
+// of the evaluation batch, the list ends at the first -1).
+template <int KMAX>
+__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
+                                                      const float* __restrict__ values) {
+  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+  if (g >= p.G) return;
+  const int K = KMAX == 1 ? 1 : p.K;
+  const int64_t row0 = (int64_t)g * K;
+  const int lane = lane_id();
+  // the slot's state and its first recorded path in one round trip (the path entries are
+  // valid memory whatever their contents; they are used only when a leaf is waiting)
+  int leaf = p.g.leaf[row0];
+  const int half = p.g.half[g];
+  int plen = p.g.path_len[row0];
+  int pn = p.g.path[row0 * kMaxPath + lane];
+  if (leaf < 0) return;
+  int done_leaf[KMAX];
+  double done_v[KMAX];
+  int n_sims = 0;
+  for (int j = 0; j < K; ++j) {
+    if (j > 0) {
+      leaf = p.g.leaf[row0 + j];
+      if (leaf < 0) break;
+      plen = p.g.path_len[row0 + j];
+      pn = p.g.path[(row0 + j) * kMaxPath + lane];
+    }
+    bool repeat = false;
+    double v_in = 0.0;
+    if constexpr (KMAX > 1) {
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (jj < j && !repeat && done_leaf[jj] == leaf) {
+          repeat = true;
+          v_in = done_v[jj];
+        }
+    }
+    const double v =
+        expand_backup_leaf(p, g, half, row0 + j, leaf, plen, pn, priors, values, repeat, v_in);
+    if (leaf != 0) ++n_sims;  // the search-start root expansion is not one of the simulations
+    if constexpr (KMAX > 1) {
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (jj == j) {
+          done_leaf[jj] = leaf;
+          done_v[jj] = v;
+        }
+      // the next leaf's path loads must see this backup's N/W stores
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+  }
   if (lane == 0) {
-    p.g.leaf[g] = -1;
+    p.g.leaf[row0] = -1;
     int sd = p.g.sims_done[g];
-    if (!is_root) {  // the search-start root expansion is not one of the simulations
-      sd += 1;
+    if (n_sims) {
+      sd += n_sims;
       p.g.sims_done[g] = sd;
-      atomicAdd(&p.ctr->sims, 1ull);
+      atomicAdd(&p.ctr->sims, (unsigned long long)n_sims);
     }
     if (sd >= p.g.sims_target[g]) {
       if (p.auto_play) push_ready(p, g);
@@ -860,7 +1020,7 @@ __device__ void new_game(const Params& p, int g) {
   p.g.winner[g] = 0;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = p.sims;
-  p.g.leaf[g] = -1;
+  p.g.leaf[(int64_t)g * p.K] = -1;
   p.g.status[g] = kActive;
 }
 
@@ -1144,7 +1304,7 @@ __global__ void k_set_root(Params p, int g, uint64_t own, uint64_t opp, int play
   init_root(p, g, 0, own, opp);
   p.g.n_nodes[g] = 1;
   p.g.root_player[g] = player;
-  p.g.leaf[g] = -1;
+  p.g.leaf[(int64_t)g * p.K] = -1;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = 0;
   p.g.status[g] = kSearchDone;
@@ -1156,7 +1316,7 @@ __global__ void k_begin(Params p, int slot, int sims) {
   if (p.g.status[g] == kIdle || p.g.status[g] == kFinished) return;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = sims;
-  p.g.leaf[g] = -1;
+  p.g.leaf[(int64_t)g * p.K] = -1;
   p.g.status[g] = kActive;
 }
 
@@ -1225,7 +1385,7 @@ __global__ void k_set_roots(Params p, const int32_t* slots, const uint64_t* own,
   init_root(p, g, 0, own[i], opp[i]);
   p.g.n_nodes[g] = 1;
   p.g.root_player[g] = player[i];
-  p.g.leaf[g] = -1;
+  p.g.leaf[(int64_t)g * p.K] = -1;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = 0;
   p.g.status[g] = kSearchDone;
@@ -1238,7 +1398,7 @@ __global__ void k_begin_slots(Params p, const int32_t* slots, int n, int sims) {
   if (g < 0 || g >= p.G) return;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = sims;
-  p.g.leaf[g] = -1;
+  p.g.leaf[(int64_t)g * p.K] = -1;
   p.g.status[g] = kActive;
 }
 
@@ -1376,6 +1536,9 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   if (cfg.sample_capacity <= 0) cfg.sample_capacity = (int64_t)cfg.n_games * cfg.max_plies * 2;
   if (cfg.inj_noise_slots <= 0) cfg.inj_noise_slots = 1;
   if (cfg.inj_uniform_slots <= 0) cfg.inj_uniform_slots = 1;
+  if (cfg.leaves_per_step <= 0) cfg.leaves_per_step = 1;
+  AZ_REQUIRE(cfg.leaves_per_step <= kMaxLeaves, AZ_ERR_ARG,
+             "leaves_per_step must be in [1, %d], got %d", kMaxLeaves, cfg.leaves_per_step);
 
   az_engine* e = new (std::nothrow) az_engine();
   AZ_REQUIRE(e, AZ_ERR_ARG, "out of host memory");
@@ -1387,6 +1550,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   p.NS = cfg.inj_noise_slots;
   p.NU = cfg.inj_uniform_slots;
   p.sims = cfg.num_simulations;
+  p.K = cfg.leaves_per_step;
   p.n_explore = cfg.num_exploratory_moves;
   p.eval_mode = cfg.eval_mode;
   p.rng_mode = cfg.rng_mode;
@@ -1424,16 +1588,17 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.g.n_nodes, G));
   chk(dalloc(e, &p.g.sims_done, G));
   chk(dalloc(e, &p.g.sims_target, G));
-  chk(dalloc(e, &p.g.leaf, G));
-  chk(dalloc(e, &p.g.path, G * kMaxPath));
-  chk(dalloc(e, &p.g.path_len, G));
+  const size_t GK = G * (size_t)p.K;
+  chk(dalloc(e, &p.g.leaf, GK));
+  chk(dalloc(e, &p.g.path, GK * kMaxPath));
+  chk(dalloc(e, &p.g.path_len, GK));
   chk(dalloc(e, &p.g.ply, G));
   chk(dalloc(e, &p.g.root_player, G));
   chk(dalloc(e, &p.g.winner, G));
   chk(dalloc(e, &p.g.overflow, G));
   chk(dalloc(e, &p.g.start_step, G));
   chk(dalloc(e, &p.g.rng_event, G));
-  chk(dalloc(e, &p.g.sym, G));
+  chk(dalloc(e, &p.g.sym, GK));
   chk(dalloc(e, &p.g.noise_cur, G));
   chk(dalloc(e, &p.g.u_cur, G));
   chk(dalloc(e, &p.g.t_own, G * T));
@@ -1487,15 +1652,16 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   // device allocation would otherwise hold a previous engine's values (out-of-range
   // halves, child ranges).
   bool zero_ok = hipMemset(p.ctr, 0, sizeof(Counters)) == hipSuccess &&
-                 hipMemset(p.g.leaf, 0xff, G * sizeof(int32_t)) == hipSuccess &&
+                 hipMemset(p.g.leaf, 0xff, GK * sizeof(int32_t)) == hipSuccess &&
+                 hipMemset(p.g.path_len, 0, GK * sizeof(int32_t)) == hipSuccess &&
                  hipMemset(p.a.flags, 0, nodes) == hipSuccess &&
                  hipMemset(p.a.nchild, 0, nodes) == hipSuccess;
   for (int32_t* a : {p.g.status, p.g.half, p.g.n_nodes, p.g.sims_done, p.g.sims_target,
-                     p.g.path_len, p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
+                     p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
                      p.g.start_step, p.g.noise_cur, p.g.u_cur})
     zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
   zero_ok = zero_ok && hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
-            hipMemset(p.g.sym, 0, G) == hipSuccess;
+            hipMemset(p.g.sym, 0, GK) == hipSuccess;
   if (!zero_ok) {
     free_all(e);
     delete e;
@@ -1562,9 +1728,16 @@ int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
     const char* v = getenv("AZ_MAX_DESCENTS");  // experiment knob (scripts/exp), default 4
     return v ? atoi(v) : 0;
   }();
-  const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4) : 4 * (e->p.sims + 1) + 64;
-  hipLaunchKernelGGL(k_select, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in, leaf_o,
-                     max_descents);
+  // (with K leaves per step the cap is 4 K descents: a step that reaches it waits on fewer
+  // leaves, another legal interleaving of the reference's workers)
+  const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4 * e->p.K)
+                                          : 4 * (e->p.sims + 1) + 64;
+  if (e->p.K == 1)
+    hipLaunchKernelGGL(k_select<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
+                       leaf_o, max_descents);
+  else
+    hipLaunchKernelGGL(k_select<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
+                       nn_in, leaf_o, max_descents);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
@@ -1574,7 +1747,12 @@ int az_expand_backup(az_engine* e, const float* priors, const float* values, voi
   AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
              "az_expand_backup: priors/values required in external-eval mode");
   hipStream_t s = azc::as_stream(stream);
-  hipLaunchKernelGGL(k_expand, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors, values);
+  if (e->p.K == 1)
+    hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
+                       values);
+  else
+    hipLaunchKernelGGL(k_expand<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
+                       priors, values);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -5,7 +5,8 @@ driver loop that replaces the reference's process-pool of `one_self_play` calls
 Per simulation step (all on one HIP stream, no host synchronisation, optionally one
 captured HIP graph):
 
-    az_select         leaves of every active game -> canonical planes nn_in [G, 64]
+    az_select         leaves of every active game -> canonical planes nn_in [G*K, 64]
+                      (K = leaves_per_step: virtual-loss descents per game per step)
     net               PyTorch-ROCm forward on nn_in -> softmax priors [G, 65], values [G]
     az_expand_backup  eager expansion + backup
     az_play           games whose search finished: pi, record, sample, move, TD(lambda)
@@ -32,7 +33,7 @@ class Engine:
                  lambd=1.0, rollout=False, injected_rng=False, d4_augment=False,
                  auto_play=True, refill=False, node_capacity=0, max_plies=0,
                  sample_capacity=0, inj_noise_slots=1, inj_uniform_slots=1, seed=0,
-                 stream_id=0, device=None):
+                 stream_id=0, device=None, leaves_per_step=1):
         if not torch.cuda.is_available():
             raise RuntimeError("the self-play engine needs a HIP device (no CPU fallback)")
         self.device = torch.device(device if device is not None else "cuda")
@@ -57,7 +58,9 @@ class Engine:
         cfg.inj_uniform_slots = int(inj_uniform_slots)
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         cfg.stream_id = int(stream_id)
+        cfg.leaves_per_step = int(leaves_per_step)
         self.cfg = cfg
+        self.K = max(1, int(leaves_per_step))
         self.rollout = rollout
         with torch.cuda.device(self.device):
             h = ctypes.c_void_p()
@@ -69,10 +72,11 @@ class Engine:
                                                  ctypes.byref(T)), "az_engine_geometry")
             self.G, self.C, self.T = G.value, C.value, T.value
             d = self.device
-            self.nn_in = torch.zeros(self.G, 64, dtype=torch.float32, device=d)
-            self.leaf = torch.full((self.G,), -1, dtype=torch.int32, device=d)
-            self.priors = torch.zeros(self.G, 65, dtype=torch.float32, device=d)
-            self.values = torch.zeros(self.G, dtype=torch.float32, device=d)
+            R = self.G * self.K  # evaluation rows: leaf j of slot g is row g*K + j
+            self.nn_in = torch.zeros(R, 64, dtype=torch.float32, device=d)
+            self.leaf = torch.full((R,), -1, dtype=torch.int32, device=d)
+            self.priors = torch.zeros(R, 65, dtype=torch.float32, device=d)
+            self.values = torch.zeros(R, dtype=torch.float32, device=d)
 
     def close(self):
         if getattr(self, "h", None):
@@ -96,8 +100,9 @@ class Engine:
     def expand(self, priors=None, values=None):
         pr = self.priors if priors is None else priors
         va = self.values if values is None else values
-        assert pr.dtype == torch.float32 and pr.is_contiguous() and pr.shape == (self.G, 65)
-        assert va.dtype == torch.float32 and va.is_contiguous() and va.numel() == self.G
+        R = self.G * self.K
+        assert pr.dtype == torch.float32 and pr.is_contiguous() and pr.shape == (R, 65)
+        assert va.dtype == torch.float32 and va.is_contiguous() and va.numel() == R
         nat.check(nat.lib.az_expand_backup(self.h, nat.ptr(pr), nat.ptr(va), self._s()),
                   "az_expand_backup")
 
@@ -254,7 +259,7 @@ class BatchedSelfPlay:
 
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
-                 device=None, fold=True, steps_per_graph=8, precision=None):
+                 device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -266,7 +271,8 @@ class BatchedSelfPlay:
             num_exploratory_moves=args.get("num_exploratory_moves", 0),
             lambd=args.get("lambda", 1.0), rollout=net is None, d4_augment=d4_augment,
             auto_play=True, refill=True, node_capacity=node_capacity,
-            sample_capacity=sample_capacity, seed=seed, stream_id=stream_id, device=device)
+            sample_capacity=sample_capacity, seed=seed, stream_id=stream_id, device=device,
+            leaves_per_step=leaves_per_step)
         self.device = self.engine.device
         if net is None:
             self.net = None

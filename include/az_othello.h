@@ -153,6 +153,11 @@ typedef struct az_config {
   int32_t inj_uniform_slots;     /* AZ_RNG_INJECTED: uniforms per slot */
   uint64_t seed;                 /* Philox key */
   uint64_t stream_id;            /* Philox sub-stream (rank) */
+  int32_t leaves_per_step;       /* K in [1, 8] (0 -> 1): leaves per slot per step, the
+                                    reference's args['num_threads'] workers with virtual loss
+                                    (MCTS_model.py:115-118, :196-197, :372-395) in one fixed
+                                    interleaving; 1 = its deterministic num_threads = 1 search.
+                                    The evaluation batch is G*K rows (row g*K + j). */
 } az_config;
 
 int az_engine_create(const az_config* cfg, az_engine** out);
@@ -174,13 +179,13 @@ int az_set_root(az_engine* eng, int32_t slot, uint64_t own, uint64_t opp, int32_
 /* start a search of num_simulations on one slot (or all, slot = -1): MCTS_model.py:237. */
 int az_begin_search(az_engine* eng, int32_t slot, int32_t num_simulations, void* stream);
 
-/* one leaf per active slot.  nn_in: float [G,64], canonical player*state (Models.py:16)
- * of the leaf, zeros for slots without a leaf.  leaf_o (optional, int32 [G]): leaf node
- * index or -1. */
+/* up to K = leaves_per_step leaves per active slot.  nn_in: float [G*K,64], canonical
+ * player*state (Models.py:16) of leaf j of slot g in row g*K + j, zeros for rows without a
+ * leaf.  leaf_o (optional, int32 [G*K]): leaf node index or -1. */
 int az_select(az_engine* eng, float* nn_in, int32_t* leaf_o, void* stream);
 
-/* priors: float [G,65] (softmax output), values: float [G] (tanh output); both ignored
- * in rollout mode. */
+/* priors: float [G*K,65] (softmax output), values: float [G*K] (tanh output), rows as
+ * az_select's; both ignored in rollout mode. */
 int az_expand_backup(az_engine* eng, const float* priors, const float* values, void* stream);
 
 /* auto-play move phase (see above); host-driven engines: step counter only. */
