@@ -5,9 +5,11 @@ and diagnostic_plots.py run unchanged.
 For OthelloGameNew the tree lives on the GPU in the batched engine's SoA node arena (one
 game slot, host-driven): each simulation is az_select (PUCT descent, wavefront argmax) ->
 policy evaluation -> az_expand_backup (eager expansion: one lane per child board step).
-The search is the reference's with args['num_threads'] = 1 — the reference's own
-deterministic mode; thread-pool virtual-loss interleaving is not
-reproduced (with 4 threads the reference is nondeterministic anyway).  Host-side draws
+args['num_threads'] (the reference's worker count, default 4, MCTS_model.py:196) becomes the
+engine's leaves_per_step K (<= 8): K virtual-loss descents per step, evaluated as one batch —
+the reference's threaded search in one fixed interleaving of its workers (pinned by goldens the
+reference itself produced under that schedule, tests/golden/make_vl_goldens.py); num_threads
+= 1 is its deterministic sequential mode.  Host-side draws
 keep the reference's np.random call order: Dirichlet root noise (np.random.dirichlet, :341)
 is injected into the engine and the temperature-0 tie break (np.random.choice, :251) is
 drawn here, so a seeded np.random reproduces the reference's search exactly (tests/).
@@ -161,6 +163,7 @@ class _EngineSearch:
         self.root_player = None
         self.dev_policy = None
         self._tree = None
+        self.K = min(8, max(1, int(args.get("num_threads", 4))))
 
     def _ensure(self):
         if self.engine is not None:
@@ -171,7 +174,8 @@ class _EngineSearch:
 
         self.engine = Engine(1, self.args["num_simulations"], c_puct=self.args["c_puct"],
                              dirichlet_alpha=self.alpha, dirichlet_epsilon=self.eps,
-                             rollout=self.policy is None, injected_rng=True, auto_play=False)
+                             rollout=self.policy is None, injected_rng=True, auto_play=False,
+                             leaves_per_step=self.K)
         if isinstance(self.policy, torch.nn.Module) and hasattr(self.policy, "evaluate_planes"):
             import copy
 
@@ -200,10 +204,17 @@ class _EngineSearch:
                     e.priors.copy_(pr)
                     e.values.copy_(va)
             return
-        canon = np.rint(e.nn_in[0].cpu().numpy()).astype(np.int8).reshape(8, 8)
-        priors, value = self.policy.inference(canon, 1)
-        e.priors[0].copy_(torch.from_numpy(np.asarray(priors, np.float32).reshape(65)))
-        e.values[0] = float(value)
+        # every waiting leaf's row (rows are packed from 0; -1 ends the list)
+        leaves = e.leaf.cpu().numpy()
+        planes = np.rint(e.nn_in.cpu().numpy()).astype(np.int8)
+        pr = np.zeros((len(leaves), 65), np.float32)
+        va = np.zeros(len(leaves), np.float32)
+        for j in np.flatnonzero(leaves >= 0):
+            priors, value = self.policy.inference(planes[j].reshape(8, 8), 1)
+            pr[j] = np.asarray(priors, np.float32).reshape(65)
+            va[j] = float(value)
+        e.priors.copy_(torch.from_numpy(pr))
+        e.values.copy_(torch.from_numpy(va))
 
     def _device_iteration(self):
         e = self.engine
@@ -251,10 +262,11 @@ class _EngineSearch:
             e.inject(noise=np.random.dirichlet([self.alpha] * 65).reshape(1, 1, 65))
         e.begin_search(0, self.args["num_simulations"])
         if self.dev_policy is not None:
-            # every select either hands out a leaf or finishes the search (its descent budget
-            # covers all simulations), so sims + 1 iterations (the root expansion included)
-            # complete it: no per-simulation host round trip
-            self._run_on_device(self.args["num_simulations"] + 1)
+            # a host-driven select always waits on min(K, remaining) leaves or finishes the
+            # search (its descent budget covers all simulations), so ceil(sims / K) + 1
+            # iterations (the root expansion included) complete it: no per-simulation host
+            # round trip (the loop below confirms)
+            self._run_on_device(-(-self.args["num_simulations"] // self.K) + 1)
         guard = 0
         while True:
             e.select()

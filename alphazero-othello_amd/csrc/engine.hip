@@ -145,6 +145,20 @@ __device__ __forceinline__ T shfl(T v, int src) {
   return __shfl(v, src, kWave);
 }
 
+// v_readlane_b32 per dword: `lane` must be wave-uniform
+template <typename T>
+__device__ __forceinline__ T readlane(T v, int lane) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "readlane: 32- or 64-bit values");
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+  }
+}
+
 // NumPy's pairwise sum of a contiguous length-65 vector (numpy/_core/src/umath/
 // loops_utils.h.src pairwise_sum: eight running partials over the first 64 elements,
 // combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail element).  x = this lane's
@@ -158,14 +172,38 @@ __device__ T np_sum65(T x, T x64) {
     const T y = shfl(x, (lane + 8 * i) & 63);
     r = r + y;
   }
-  const T r0 = shfl(r, 0), r1 = shfl(r, 1), r2 = shfl(r, 2), r3 = shfl(r, 3);
-  const T r4 = shfl(r, 4), r5 = shfl(r, 5), r6 = shfl(r, 6), r7 = shfl(r, 7);
+  const T r0 = readlane(r, 0), r1 = readlane(r, 1), r2 = readlane(r, 2), r3 = readlane(r, 3);
+  const T r4 = readlane(r, 4), r5 = readlane(r, 5), r6 = readlane(r, 6), r7 = readlane(r, 7);
   T res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
   res = res + x64;
   return res;
 }
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
+
+// Wave argmax with Python max()'s tie rule (the first maximum, i.e. the lowest lane):
+// the scores become order-preserving unsigned keys (-0 folded into +0, as a float compare
+// sees them; absent lanes 0), the wave maximum comes from the DPP reduction
+// __ockl_wfred_max_u32 (VALU data-parallel moves, no LDS round trips), and the lowest lane
+// holding it from a ballot.  Called with the whole wave active.
+__device__ __forceinline__ uint32_t order_key32(float s) {
+  const uint32_t b = __float_as_uint(s + 0.0f);
+  return b ^ ((b >> 31) ? 0xffffffffu : 0x80000000u);
+}
+__device__ __forceinline__ int wave_argmax_f32(float s, bool live) {
+  const uint32_t key = live ? order_key32(s) : 0u;
+  const uint32_t m = __ockl_wfred_max_u32(key);
+  return (int)__builtin_ctzll(ballot(live && key == m));
+}
+__device__ __forceinline__ int wave_argmax_f64(double s, bool live) {
+  const uint64_t b = (uint64_t)__double_as_longlong(s + 0.0);
+  const uint64_t key = live ? (b ^ ((b >> 63) ? ~0ull : 0x8000000000000000ull)) : 0ull;
+  const uint32_t hi = (uint32_t)(key >> 32), lo = (uint32_t)key;
+  const uint32_t mh = __ockl_wfred_max_u32(hi);
+  const uint32_t ml = __ockl_wfred_max_u32(hi == mh ? lo : 0u);
+  return (int)__builtin_ctzll(ballot(live && hi == mh && lo == ml));
+}
+
 
 // ---------------------------------------------------------------------------------
 // node helpers (executed by the whole wave; stores by lane 0 only where noted)
@@ -258,20 +296,22 @@ __device__ __forceinline__ int rec_tval(const NodeRec& r) { return (int)(int8_t)
 // sqrt is float32 (c_puct and q are cast to float32); with the Dirichlet-noised root's
 // float64 priors it is all float64.  The node's own virtual visit (+1, MCTS_model.py:378)
 // enters the sqrt; the children carry none.  max() keeps the first maximum in ascending
-// action order, i.e. the lowest child index.
+// action order, i.e. the lowest child index (wave_argmax_*).
 // The parent's record is already in registers, each lane
-// loads its child's PUCT inputs AND its record, and the winner's record is broadcast from
-// its lane -- the next level starts without another load.
+// loads its child's PUCT inputs AND its record, and the winner's record is read from its
+// lane (v_readlane: the winner is wave-uniform) -- the next level starts without another
+// load.
 __device__ NodeRec select_child_rec(const Params& p, int g, int half, const NodeRec& par) {
   const int lane = lane_id();
   const int nc = rec_nchild(par);
   const int fc = par.first;
   const bool f64 = (rec_flags(par) & kChildF64) != 0;
   const double sq = sqrt((double)(par.visits + 1) + 1e-8);
-  double score = -INFINITY;
-  int idx = 0x7fffffff;
+  const bool live = lane < nc;
   NodeRec mine{0, 0, 0, 0, 0ull, 0ull};
-  if (lane < nc) {
+  double sd = 0.0;
+  float sf = 0.0f;
+  if (live) {
     const int64_t c = nidx(p, half, g, fc + lane);
     const int n = p.a.N[c];
     const double w = p.a.W[c];
@@ -284,29 +324,20 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
     const double q = -(n == 0 ? 0.0 : w / (double)n);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + n);
-      score = q + u;
+      sd = q + u;
     } else {
       const float u = (((float)p.c_puct * (float)pr) * (float)sq) / (float)(1 + n);
-      score = (double)((float)q + u);
-    }
-    idx = lane;
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double os = __shfl_xor(score, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    if (os > score || (os == score && oi < idx)) {
-      score = os;
-      idx = oi;
+      sf = (float)q + u;
     }
   }
+  const int idx = f64 ? wave_argmax_f64(sd, live) : wave_argmax_f32(sf, live);
   NodeRec r;
   r.node = fc + idx;
-  r.first = __shfl(mine.first, idx, kWave);
-  r.visits = __shfl(mine.visits, idx, kWave);
-  r.meta = __shfl(mine.meta, idx, kWave);
-  r.own = __shfl(mine.own, idx, kWave);
-  r.opp = __shfl(mine.opp, idx, kWave);
+  r.first = readlane(mine.first, idx);
+  r.visits = readlane(mine.visits, idx);
+  r.meta = readlane(mine.meta, idx);
+  r.own = readlane(mine.own, idx);
+  r.opp = readlane(mine.opp, idx);
   return r;
 }
 
@@ -333,7 +364,7 @@ __device__ __forceinline__ int virtual_visits(const Waiting<KMAX>& w, int depth,
   int c = 0;
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
-    if (j < w.n) c += __shfl(w.path[j], depth, kWave) == node ? 1 : 0;
+    if (j < w.n) c += readlane(w.path[j], depth) == node ? 1 : 0;
   return c;
 }
 
@@ -350,10 +381,11 @@ __device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeR
   const int vvp = 1 + virtual_visits(w, depth, par.node);
   const double sq = sqrt((double)(par.visits + vvp) + 1e-8);
   const int vvc = depth + 1 < kMaxPath ? virtual_visits(w, depth + 1, fc + lane) : 0;
-  double score = -INFINITY;
-  int idx = 0x7fffffff;
+  const bool live = lane < nc;
   NodeRec mine{0, 0, 0, 0, 0ull, 0ull};
-  if (lane < nc) {
+  double sd = 0.0;
+  float sf = 0.0f;
+  if (live) {
     const int64_t c = nidx(p, half, g, fc + lane);
     const int n = p.a.N[c];
     const double wv = p.a.W[c];
@@ -367,29 +399,20 @@ __device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeR
     const double q = -(nv == 0 ? 0.0 : (wv + (double)vvc) / (double)nv);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + nv);
-      score = q + u;
+      sd = q + u;
     } else {
       const float u = (((float)p.c_puct * (float)pr) * (float)sq) / (float)(1 + nv);
-      score = (double)((float)q + u);
-    }
-    idx = lane;
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double os = __shfl_xor(score, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    if (os > score || (os == score && oi < idx)) {
-      score = os;
-      idx = oi;
+      sf = (float)q + u;
     }
   }
+  const int idx = f64 ? wave_argmax_f64(sd, live) : wave_argmax_f32(sf, live);
   NodeRec r;
   r.node = fc + idx;
-  r.first = __shfl(mine.first, idx, kWave);
-  r.visits = __shfl(mine.visits, idx, kWave);
-  r.meta = __shfl(mine.meta, idx, kWave);
-  r.own = __shfl(mine.own, idx, kWave);
-  r.opp = __shfl(mine.opp, idx, kWave);
+  r.first = readlane(mine.first, idx);
+  r.visits = readlane(mine.visits, idx);
+  r.meta = readlane(mine.meta, idx);
+  r.own = readlane(mine.own, idx);
+  r.opp = readlane(mine.opp, idx);
   return r;
 }
 
@@ -574,7 +597,7 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t r
       pr64 = 1.0f;
       double vv = 0.0;
       if (lane == 0) vv = rollout(p, g, own, opp);
-      v = shfl(vv, 0);
+      v = readlane(vv, 0);
     } else {
       const float* prow = priors + row * 65;
       const int sym = p.d4 ? p.g.sym[row] : 0;
@@ -645,7 +668,7 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t r
         atomicAdd(&p.ctr->overflow, 1ull);
       }
     }
-    fc = shfl(fc, 0);
+    fc = readlane(fc, 0);
     if (fc >= 0) {
       const bool mine = lg ? valid : (lane == 0);
       const int a = lg ? lane : azb::kPass;

@@ -91,6 +91,9 @@ def parse():
                          "(32,768 on 8 GPUs, RCCL all-gather); c5 = configs[4], c4 + fused D4 "
                          "symmetry per leaf + fp16 inference")
     ap.add_argument("--games", type=int, default=None, help="concurrent games per GPU")
+    ap.add_argument("--leaves", type=int, default=1,
+                    help="virtual-loss leaves per game per step (the reference's num_threads; "
+                         "SURVEY 8d C3 allows 256 games x 4 leaves = a 1,024-row leaf batch)")
     ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--net", default=None, choices=["az5x128", "fast"])
     ap.add_argument("--conv-precision", default=None, choices=["fp16x2", "split3", "fp32", "fp16"],
@@ -473,11 +476,11 @@ def main():
                          use_graph=not a.no_graph, device=device, d4_augment=a.d4,
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
                          sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
-                         precision=a.conv_precision)
+                         precision=a.conv_precision, leaves_per_step=a.leaves)
     e = sp.engine
     # stagger slot starts over one game length: at the end of the warmup every slot plays
     # and the game phases are uniform (steady state of continuous self-play)
-    stagger = (a.sims + 1) * int(REF_PLIES_PER_GAME)
+    stagger = (-(-a.sims // a.leaves) + 1) * int(REF_PLIES_PER_GAME)
     warmup_run = a.warmup if a.warmup_exact else max(a.warmup, stagger)
     sp.reset(start_budget=-1, stagger_steps=stagger)
 
@@ -556,6 +559,7 @@ def main():
                                       "symmetry per leaf + fp16 net inference"}[a.workload],
                    "d4_augment": a.d4,
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
+                   "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
                    "hip_graph": sp.graph is not None},
         "value_basis": basis,
@@ -592,7 +596,7 @@ def main():
                                                            / 1e9 / HBM_PEAK_GBS, 4)}
     if rank == 0 and not a.skip_kernel and hasattr(sp.net, "c2") \
             and getattr(sp.net, "conv_impl", "") == "hip":
-        result["roofline_conv"] = conv_roofline(sp, device, a.games)
+        result["roofline_conv"] = conv_roofline(sp, device, a.games * a.leaves)
     if rank == 0 and not a.skip_cpu:
         result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds, a.cpu_workers)
     if rank == 0:

@@ -7,6 +7,9 @@
     game, games/s and ms per move;
   * arena: eval.py:134-178 play_match's per-move call, `policy_improve_step(temp=0)` +
     `make_move` on two drop-in MCTS (two nets), ms per move over one game.
+Both with the callers' own args -- train.py:399-423 / eval.py:191 pass no num_threads, so
+the reference default of 4 workers (MCTS_model.py:196) = 4 virtual-loss leaves per engine
+step -- and with num_threads = 1 (the sequential search).
 One JSON line.  The batched engine (bench.py) is the production path; this measures what a
 caller gets without changing a line."""
 import json
@@ -25,14 +28,15 @@ from envs.othello import OthelloGameNew  # noqa: E402
 import self_play_worker  # noqa: E402
 
 
-def main():
-    sims = int(os.environ.get("SIMS", 400))
+def run(threads, sims):
     torch.manual_seed(0)
     np.random.seed(0)
     net = AlphaZeroNet(8, 65, 5, 128).eval()
-    args = {"c_puct": 2.0, "num_simulations": sims, "num_threads": 1, "dirichlet_alpha": 1.0,
-            "dirichlet_epsilon": 0.25, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
+    args = {"c_puct": 2.0, "num_simulations": sims, "dirichlet_alpha": 1.0,
+            "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
             "lambda": 0.98}
+    if threads is not None:
+        args["num_threads"] = threads
     ps = (AlphaZeroNet, {"board_size": 8, "action_size": 65, "n_res_blocks": 5, "channels": 128},
           net.state_dict())
     # warm-up game (captures the graphs, loads the kernels)
@@ -49,7 +53,9 @@ def main():
     # eval.py play_match's per-move loop on two drop-in MCTS
     env = OthelloGameNew(8)
     net2 = AlphaZeroNet(8, 65, 5, 128).eval()
-    a = {"c_puct": 2.0, "num_simulations": sims, "num_threads": 1}
+    a = {"c_puct": 2.0, "num_simulations": sims}
+    if threads is not None:
+        a["num_threads"] = threads
     players = {1: MCTS(env, a, net), -1: MCTS(env, a, net2)}
     state, player, moves, t = env.get_initial_state(), 1, 0, 0.0
     while True:
@@ -67,7 +73,13 @@ def main():
         player = -player
     res["arena_play_match"] = {"ms_per_move": round(t / moves * 1e3, 2), "moves": moves,
                                "sims": sims}
-    res["device"] = torch.cuda.get_device_name(0)
+    return res
+
+
+def main():
+    sims = int(os.environ.get("SIMS", 400))
+    res = {"num_threads_default_4": run(None, sims), "num_threads_1": run(1, sims),
+           "device": torch.cuda.get_device_name(0)}
     print(json.dumps(res))
 
 

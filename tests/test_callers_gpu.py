@@ -7,8 +7,10 @@ on the bot's turns, the opponent's move chosen outside MCTS, `mcts.make_move(a)`
 EVERY ply (both sides, tree reuse), and `(mcts.root.value + 1) / 2 if mcts.root` read as
 the win probability.  Here the opponent is a seeded random legal mover (the human / the
 Egaroucid engine stand-in) and the net is the deterministic mock policy; the expected
-moves and root values come from the oracle's sequential restatement of the reference
-MCTS (oracle/mcts.py, pinned to reference-run goldens), with np.random seeded identically
+moves and root values come from the oracle's restatement of the reference MCTS
+(oracle/mcts.py, pinned to reference-run goldens) -- with the reference's default of 4
+worker threads (MCTS_model.py:196: these callers pass no num_threads), i.e. the 4-leaf
+virtual-loss search (tests/golden/make_vl_goldens.py) -- with np.random seeded identically
 before every search (temp 0 breaks count ties with np.random.choice, MCTS_model.py:247).
 Bit-exact: every bot move, every root value and visit count."""
 import numpy as np
@@ -35,7 +37,7 @@ def _play(bot_player, sims, seed):
     env = OthelloGameNew(8)
     args = {"c_puct": 3.0, "num_simulations": sims}  # play_othello.py:41's keys
     mcts = MCTS(env, args, MockPolicy(), apply_symmetry=True)
-    ref = SeqMCTS(args["c_puct"], sims, _oracle_eval)
+    ref = SeqMCTS(args["c_puct"], sims, _oracle_eval, leaves_per_step=4)
     opp_rng = np.random.default_rng(seed)
     game = ob.OracleGame()
     state, ostate = env.get_initial_state(), game.get_initial_state()
