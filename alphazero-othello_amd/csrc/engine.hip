@@ -291,6 +291,36 @@ __device__ __forceinline__ uint8_t rec_flags(const NodeRec& r) { return (uint8_t
 __device__ __forceinline__ int rec_nchild(const NodeRec& r) { return (r.meta >> 8) & 0xff; }
 __device__ __forceinline__ int rec_tval(const NodeRec& r) { return (int)(int8_t)(r.meta >> 16); }
 
+// One child's PUCT inputs and record (a select_child lane's loads).
+struct KidIn {
+  int n, first, meta;
+  double w, pr;
+  uint64_t own, opp;
+};
+
+__device__ __forceinline__ KidIn load_kid(const Params& p, int g, int half, int node) {
+  const int64_t c = nidx(p, half, g, node);
+  KidIn k;
+  k.n = p.a.N[c];
+  k.w = p.a.W[c];
+  k.pr = p.a.P[c];
+  k.first = p.a.first[c];
+  k.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
+  k.own = p.a.own[c];
+  k.opp = p.a.opp[c];
+  return k;
+}
+
+// The root's record together with its children's (one round trip): an expanded root's
+// children are always nodes 1..nchild -- the root expands into the arena's second slot, and
+// the stable re-root compaction keeps a subtree root's child group right behind it -- so
+// lane j loads node 1 + j speculatively (in bounds: C >= 128); select_child_rec checks
+// first == 1 before using them.
+__device__ __forceinline__ NodeRec load_root(const Params& p, int g, int half, KidIn& kid) {
+  kid = load_kid(p, g, half, 1 + lane_id());
+  return load_rec(p, g, half, 0);
+}
+
 // PUCT child choice of MCTS._select_child / Node._get_ucb_score (MCTS_model.py:129-139,
 // :362-370).  NumPy-2 promotion: with float32 priors every operation after the Python-float
 // sqrt is float32 (c_puct and q are cast to float32); with the Dirichlet-noised root's
@@ -301,7 +331,8 @@ __device__ __forceinline__ int rec_tval(const NodeRec& r) { return (int)(int8_t)
 // loads its child's PUCT inputs AND its record, and the winner's record is read from its
 // lane (v_readlane: the winner is wave-uniform) -- the next level starts without another
 // load.
-__device__ NodeRec select_child_rec(const Params& p, int g, int half, const NodeRec& par) {
+__device__ NodeRec select_child_rec(const Params& p, int g, int half, const NodeRec& par,
+                                   bool use_pre, const KidIn& pre) {
   const int lane = lane_id();
   const int nc = rec_nchild(par);
   const int fc = par.first;
@@ -312,15 +343,15 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
   double sd = 0.0;
   float sf = 0.0f;
   if (live) {
-    const int64_t c = nidx(p, half, g, fc + lane);
-    const int n = p.a.N[c];
-    const double w = p.a.W[c];
-    const double pr = p.a.P[c];
-    mine.first = p.a.first[c];
-    mine.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
+    const KidIn k = use_pre && fc == 1 ? pre : load_kid(p, g, half, fc + lane);
+    const int n = k.n;
+    const double w = k.w;
+    const double pr = k.pr;
+    mine.first = k.first;
+    mine.meta = k.meta;
     mine.visits = n;
-    mine.own = p.a.own[c];
-    mine.opp = p.a.opp[c];
+    mine.own = k.own;
+    mine.opp = k.opp;
     const double q = -(n == 0 ? 0.0 : w / (double)n);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + n);
@@ -373,7 +404,8 @@ __device__ __forceinline__ int virtual_visits(const Waiting<KMAX>& w, int depth,
 // 110-114, :129-139).  With no waiting descent this is select_child_rec's arithmetic.
 template <int KMAX>
 __device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeRec& par,
-                                   int depth, const Waiting<KMAX>& w) {
+                                   int depth, const Waiting<KMAX>& w, bool use_pre,
+                                   const KidIn& pre) {
   const int lane = lane_id();
   const int nc = rec_nchild(par);
   const int fc = par.first;
@@ -386,15 +418,15 @@ __device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeR
   double sd = 0.0;
   float sf = 0.0f;
   if (live) {
-    const int64_t c = nidx(p, half, g, fc + lane);
-    const int n = p.a.N[c];
-    const double wv = p.a.W[c];
-    const double pr = p.a.P[c];
-    mine.first = p.a.first[c];
-    mine.meta = (int)p.a.flags[c] | ((int)p.a.nchild[c] << 8) | ((int)(uint8_t)p.a.tval[c] << 16);
+    const KidIn k = use_pre && fc == 1 ? pre : load_kid(p, g, half, fc + lane);
+    const int n = k.n;
+    const double wv = k.w;
+    const double pr = k.pr;
+    mine.first = k.first;
+    mine.meta = k.meta;
     mine.visits = n;
-    mine.own = p.a.own[c];
-    mine.opp = p.a.opp[c];
+    mine.own = k.own;
+    mine.opp = k.opp;
     const int nv = n + vvc;
     const double q = -(nv == 0 ? 0.0 : (wv + (double)vvc) / (double)nv);
     if (f64) {
@@ -447,7 +479,8 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   bool deep = false;  // a waiting path past kMaxPath: its virtual loss could not be tracked
   int depth = 0;      // depth of the current node
   int path_node = 0;  // lane d: node at depth d of the current descent
-  NodeRec cur = load_rec(p, g, half, 0);
+  KidIn kid0;  // the root's children (load_root)
+  NodeRec cur = load_root(p, g, half, kid0);
   // the leaf in `cur` waits for evaluation as row g*K + w.n
   auto wait_leaf = [&]() {
     const int j = w.n;
@@ -482,7 +515,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   } else {
     int guard = 0;
     while (sims_done + w.n < target && w.n < K && guard < max_descents) {
-      if (guard > 0) cur = load_rec(p, g, half, 0);  // the last backup changed the root's N
+      if (guard > 0) cur = load_root(p, g, half, kid0);  // the last backup changed the root's N
       ++guard;
       depth = 0;
       path_node = 0;
@@ -505,9 +538,9 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
           break;
         }
         if constexpr (KMAX == 1) {
-          cur = select_child_rec(p, g, half, cur);
+          cur = select_child_rec(p, g, half, cur, depth == 0, kid0);
         } else {
-          cur = select_child_vl<KMAX>(p, g, half, cur, depth, w);
+          cur = select_child_vl<KMAX>(p, g, half, cur, depth, w, depth == 0, kid0);
         }
         ++depth;
         if (lane == depth) path_node = cur.node;
@@ -571,10 +604,35 @@ __device__ double rollout(const Params& p, int g, uint64_t own, uint64_t opp) {
 // leaf -- it is expanded already and this descent only backs up that descent's value `v_in`
 // (two reference workers on one leaf both expand it, the second with identical fresh
 // children, and both back up).  Returns the value backed up.
-__device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t row, int leaf,
-                                     int plen, int pn, const float* __restrict__ priors,
-                                     const float* __restrict__ values, bool repeat,
-                                     double v_in) {
+// What a waiting leaf's expansion reads that does not depend on the tree: loaded for every
+// leaf of the slot in the kernel's first round trip.
+struct LeafIn {
+  int leaf, plen, pn;  // node, recorded path length, lane's path entry
+  float pr, pr64, v;   // evaluation row: this lane's prior (row order), prior 64, value
+  int sym;             // D4 transform the leaf was packed through
+};
+
+__device__ __forceinline__ LeafIn load_leaf_in(const Params& p, int64_t row,
+                                               const float* __restrict__ priors,
+                                               const float* __restrict__ values) {
+  const int lane = lane_id();
+  LeafIn in;
+  in.leaf = p.g.leaf[row];
+  in.plen = p.g.path_len[row];
+  in.pn = p.g.path[row * kMaxPath + lane];
+  // (rollout mode: the host passes a zeroed stand-in buffer, so the loads need no branch)
+  in.pr = priors[row * 65 + lane];
+  in.pr64 = priors[row * 65 + 64];
+  in.v = values[row];
+  in.sym = p.g.sym[row];  // meaningful only with p.d4 (the caller masks it)
+  return in;
+}
+
+// n_nodes: the slot's allocation cursor, carried in a register across the step's leaves
+// (lane-uniform) and stored once by the caller.
+__device__ double expand_backup_leaf(const Params& p, int g, int half, const LeafIn& in,
+                                     int& n_nodes, bool repeat, double v_in) {
+  const int leaf = in.leaf, plen = in.plen, pn = in.pn;
   const int lane = lane_id();
   const int64_t k = nidx(p, half, g, leaf);
   const uint64_t own = p.a.own[k], opp = p.a.opp[k], lg = p.a.legal[k];
@@ -599,12 +657,11 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t r
       if (lane == 0) vv = rollout(p, g, own, opp);
       v = readlane(vv, 0);
     } else {
-      const float* prow = priors + row * 65;
-      const int sym = p.d4 ? p.g.sym[row] : 0;
-      // unsymmetrise_pi (MCTS_model.py:31-43): the net saw the board through `sym`
-      pr = prow[sym ? azb::d4_square(lane, sym) : lane];
-      pr64 = prow[64];
-      v = (double)values[row];
+      // unsymmetrise_pi (MCTS_model.py:31-43): the net saw the board through `sym`, so
+      // lane a takes the row entry of square d4(a)
+      pr = in.sym ? __shfl(in.pr, azb::d4_square(lane, in.sym), kWave) : in.pr;
+      pr64 = in.pr64;
+      v = (double)in.v;
     }
     const bool valid = lg ? ((lg >> lane) & 1) != 0 : false;
     const bool valid64 = lg == 0;
@@ -657,18 +714,16 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, int64_t r
 
     // ---- eager expansion of every legal child (MCTS_model.py:352-357, :146-158)
     const int nc = lg ? azb::popc(lg) : 1;
-    int fc = 0;
-    if (lane == 0) {
-      fc = p.g.n_nodes[g];
-      if (fc + nc <= p.C) {
-        p.g.n_nodes[g] = fc + nc;
-      } else {
-        fc = -1;
+    int fc = n_nodes;
+    if (fc + nc <= p.C) {
+      n_nodes = fc + nc;
+    } else {
+      fc = -1;
+      if (lane == 0) {
         p.g.overflow[g] += 1;
         atomicAdd(&p.ctr->overflow, 1ull);
       }
     }
-    fc = readlane(fc, 0);
     if (fc >= 0) {
       const bool mine = lg ? valid : (lane == 0);
       const int a = lg ? lane : azb::kPass;
@@ -727,56 +782,57 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
   const int K = KMAX == 1 ? 1 : p.K;
   const int64_t row0 = (int64_t)g * K;
   const int lane = lane_id();
-  // the slot's state and its first recorded path in one round trip (the path entries are
-  // valid memory whatever their contents; they are used only when a leaf is waiting)
-  int leaf = p.g.leaf[row0];
+  // one round trip for everything that does not depend on the tree: the slot's words and,
+  // for every waiting leaf, its recorded path and evaluation row (the rows are valid memory
+  // whatever they hold; they are used only for leaves that wait)
   const int half = p.g.half[g];
-  int plen = p.g.path_len[row0];
-  int pn = p.g.path[row0 * kMaxPath + lane];
-  if (leaf < 0) return;
-  int done_leaf[KMAX];
+  int n_nodes = p.g.n_nodes[g];
+  const int sd0 = p.g.sims_done[g], target = p.g.sims_target[g];
+  LeafIn in[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j < K) in[j] = load_leaf_in(p, row0 + j, priors, values);
+  // every load above in flight before any is waited for (the compiler would otherwise sink
+  // them past the early exit below, one dependent round trip each)
+  asm volatile("" ::"v"(half), "v"(n_nodes), "v"(sd0), "v"(target));
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j < K)
+      asm volatile("" ::"v"(in[j].leaf), "v"(in[j].plen), "v"(in[j].pn), "v"(in[j].pr),
+                   "v"(in[j].pr64), "v"(in[j].v), "v"(in[j].sym));
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) in[j].sym = p.d4 ? in[j].sym : 0;
+  if (in[0].leaf < 0) return;
   double done_v[KMAX];
   int n_sims = 0;
-  for (int j = 0; j < K; ++j) {
-    if (j > 0) {
-      leaf = p.g.leaf[row0 + j];
-      if (leaf < 0) break;
-      plen = p.g.path_len[row0 + j];
-      pn = p.g.path[(row0 + j) * kMaxPath + lane];
-    }
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    if (j >= K || in[j].leaf < 0) break;
+    const int leaf = in[j].leaf;
+    // a leaf an earlier descent of this step waits on too: expanded already, this descent
+    // only backs up that value
     bool repeat = false;
     double v_in = 0.0;
-    if constexpr (KMAX > 1) {
 #pragma unroll
-      for (int jj = 0; jj < KMAX; ++jj)
-        if (jj < j && !repeat && done_leaf[jj] == leaf) {
-          repeat = true;
-          v_in = done_v[jj];
-        }
-    }
-    const double v =
-        expand_backup_leaf(p, g, half, row0 + j, leaf, plen, pn, priors, values, repeat, v_in);
+    for (int jj = 0; jj < j; ++jj)
+      if (!repeat && in[jj].leaf == leaf) {
+        repeat = true;
+        v_in = done_v[jj];
+      }
+    done_v[j] = expand_backup_leaf(p, g, half, in[j], n_nodes, repeat, v_in);
     if (leaf != 0) ++n_sims;  // the search-start root expansion is not one of the simulations
-    if constexpr (KMAX > 1) {
-#pragma unroll
-      for (int jj = 0; jj < KMAX; ++jj)
-        if (jj == j) {
-          done_leaf[jj] = leaf;
-          done_v[jj] = v;
-        }
-      // the next leaf's path loads must see this backup's N/W stores
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    }
+    // the next leaf's path loads must see this backup's N/W stores
+    if (KMAX > 1) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   if (lane == 0) {
     p.g.leaf[row0] = -1;
-    int sd = p.g.sims_done[g];
+    p.g.n_nodes[g] = n_nodes;
+    const int sd = sd0 + n_sims;
     if (n_sims) {
-      sd += n_sims;
       p.g.sims_done[g] = sd;
       atomicAdd(&p.ctr->sims, (unsigned long long)n_sims);
     }
-    if (sd >= p.g.sims_target[g]) {
+    if (sd >= target) {
       if (p.auto_play) push_ready(p, g);
       else p.g.status[g] = kSearchDone;
     }
@@ -914,27 +970,29 @@ __device__ int sample_action(const float* pis, double u) {
 // instead of a level-by-level BFS: a handful of global round trips per re-root, not two per
 // tree level.  Whole workgroup; `scratch` = LDS of p.C ints, used as two u16 arrays (node
 // offsets from `child` are < p.C <= 32768, 0xffff = not in the subtree).
-__device__ int compact(const Params& p, int g, int child, int32_t* scratch) {
+__device__ int compact(const Params& p, int g, int child, int32_t* scratch, int oh,
+                       int n_nodes) {
   constexpr uint16_t kOut = 0xffff;
-  constexpr int kU = 8;  // parent loads in flight per thread
+  constexpr int kU = 8;   // LDS link reads in flight per thread (pointer jumping)
+  constexpr int kP = 32;  // parent loads in flight per thread (one round trip per 8,192 nodes)
   __shared__ int s_scan[kMoveBlock / kWave];
   uint16_t* rel = reinterpret_cast<uint16_t*>(scratch);  // old offset -> link, then new index
   uint16_t* inv = rel + p.C;                             // new index -> old offset
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int oh = p.g.half[g], nh = oh ^ 1;
-  const int span = p.g.n_nodes[g] - child;  // candidates: old nodes child .. n_nodes-1
+  const int nh = oh ^ 1;
+  const int span = n_nodes - child;  // candidates: old nodes child .. n_nodes-1
   // 1. rel[j] = parent of old node child+j as an offset from `child` (descendants of `child`
   // all lie above it; a parent below it means "not in the subtree")
-  for (int j0 = 0; j0 < span; j0 += kMoveBlock * kU) {
-    int par[kU];
+  for (int j0 = 0; j0 < span; j0 += kMoveBlock * kP) {
+    int par[kP];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kP; ++u) {
       const int j = j0 + u * kMoveBlock + tid;
       par[u] = (j > 0 && j < span) ? p.a.parent[nidx(p, oh, g, child + j)] : child;
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kP; ++u) {
       const int j = j0 + u * kMoveBlock + tid;
       if (j < span) rel[j] = par[u] >= child ? (uint16_t)(par[u] - child) : kOut;
     }
@@ -994,26 +1052,54 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch) {
     }
   }
   __syncthreads();
-  // 4. copy the members, translating parent / first-child links
-  for (int i = tid; i < n_new; i += kMoveBlock) {
-    const int j = inv[i];
-    const int64_t ok = nidx(p, oh, g, child + j);
-    const int64_t nk = nidx(p, nh, g, i);
-    const uint8_t f = p.a.flags[ok];
-    const bool ex = (f & kExpanded) != 0;
-    const int par = p.a.parent[ok], fc = p.a.first[ok];
-    p.a.own[nk] = p.a.own[ok];
-    p.a.opp[nk] = p.a.opp[ok];
-    p.a.legal[nk] = p.a.legal[ok];
-    p.a.N[nk] = p.a.N[ok];
-    p.a.W[nk] = p.a.W[ok];
-    p.a.P[nk] = p.a.P[ok];
-    p.a.action[nk] = p.a.action[ok];
-    p.a.flags[nk] = f;
-    p.a.tval[nk] = p.a.tval[ok];
-    p.a.nchild[nk] = ex ? p.a.nchild[ok] : (uint8_t)0;
-    p.a.first[nk] = ex ? (int)rel[fc - child] : -1;
-    p.a.parent[nk] = i == 0 ? -1 : (int)rel[par - child];
+  // 4. copy the members, translating parent / first-child links: kC nodes per thread with
+  // every load issued before the first store (one global round trip per kC * block nodes
+  // instead of one per block of nodes)
+  constexpr int kC = 4;
+  for (int i0 = tid; i0 < n_new; i0 += kMoveBlock * kC) {
+    uint64_t own[kC], opp[kC], lg[kC];
+    double W[kC], P[kC];
+    int N[kC], par[kC], fc[kC];
+    uint8_t act[kC], fl[kC], tv[kC], nch[kC];
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int i = i0 + u * kMoveBlock;
+      if (i < n_new) {
+        const int64_t ok = nidx(p, oh, g, child + inv[i]);
+        own[u] = p.a.own[ok];
+        opp[u] = p.a.opp[ok];
+        lg[u] = p.a.legal[ok];
+        N[u] = p.a.N[ok];
+        W[u] = p.a.W[ok];
+        P[u] = p.a.P[ok];
+        act[u] = p.a.action[ok];
+        fl[u] = p.a.flags[ok];
+        tv[u] = p.a.tval[ok];
+        nch[u] = p.a.nchild[ok];
+        par[u] = p.a.parent[ok];
+        fc[u] = p.a.first[ok];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int i = i0 + u * kMoveBlock;
+      if (i < n_new) {
+        const int64_t nk = nidx(p, nh, g, i);
+        const bool ex = (fl[u] & kExpanded) != 0;
+        p.a.own[nk] = own[u];
+        p.a.opp[nk] = opp[u];
+        p.a.legal[nk] = lg[u];
+        p.a.N[nk] = N[u];
+        p.a.W[nk] = W[u];
+        p.a.P[nk] = P[u];
+        p.a.action[nk] = act[u];
+        p.a.flags[nk] = fl[u];
+        p.a.tval[nk] = tv[u];
+        p.a.nchild[nk] = ex ? nch[u] : (uint8_t)0;
+        p.a.first[nk] = ex ? (int)rel[fc[u] - child] : -1;
+        p.a.parent[nk] = i == 0 ? -1 : (int)rel[par[u] - child];
+      }
+    }
   }
   if (tid == 0) {
     p.g.half[g] = nh;
@@ -1142,24 +1228,32 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
     const int half = p.g.half[g];
     const int ply = p.g.ply[g];
     const int player = p.g.root_player[g];
+    const int n_nodes = p.g.n_nodes[g];
     if (tid < 64) {
-      // ---- one round trip for the root record and the slot's RNG cursor, one for the
-      // children's records (lane j = child j); everything after works from registers
+      // ---- one round trip for the root record, the children's records (lane j = child j,
+      // nodes 1 + j: load_root) and the slot's RNG cursor; everything after works from
+      // registers
       const int64_t r = nidx(p, half, g, 0);
+      const int64_t ck = nidx(p, half, g, 1 + tid);
+      int c_n = p.a.N[ck], c_flags = p.a.flags[ck];
+      uint64_t c_own = p.a.own[ck], c_opp = p.a.opp[ck];
       const int nc = p.a.nchild[r], fc = p.a.first[r];
       const uint64_t lg = p.a.legal[r], r_own = p.a.own[r], r_opp = p.a.opp[r];
       const int r_n = p.a.N[r];
       const double r_w = p.a.W[r];
       const bool injected = p.rng_mode == AZ_RNG_INJECTED;
       const uint32_t rng0 = injected ? (uint32_t)p.g.u_cur[g] : p.g.rng_event[g];
-      int c_n = 0, c_flags = 0;
-      uint64_t c_own = 0, c_opp = 0;
-      if (tid < nc) {
-        const int64_t ck = nidx(p, half, g, fc + tid);
-        c_n = p.a.N[ck];
-        c_flags = p.a.flags[ck];
-        c_own = p.a.own[ck];
-        c_opp = p.a.opp[ck];
+      if (fc != 1 && tid < nc) {  // not reached (see load_root); kept for safety
+        const int64_t ck2 = nidx(p, half, g, fc + tid);
+        c_n = p.a.N[ck2];
+        c_flags = p.a.flags[ck2];
+        c_own = p.a.own[ck2];
+        c_opp = p.a.opp[ck2];
+      }
+      if (tid >= nc) {
+        c_n = 0;
+        c_flags = 0;
+        c_own = c_opp = 0;
       }
       // ---- the move's uniform draws (next_uniform, in draw order): the tie-break draw
       // when temp < 0.1, then the action sample
@@ -1259,7 +1353,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
       __syncthreads();
       if (s_restart && tid == 0) new_game(p, g);
     } else {
-      compact(p, g, s_child, map);
+      compact(p, g, s_child, map, half, n_nodes);
       if (tid == 0) {
         p.g.ply[g] = ply + 1;
         p.g.root_player[g] = -player;
@@ -1387,7 +1481,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_reroot(Params p, int g, int acti
   __syncthreads();
   if (s_child < 0) return;
   const int player = p.g.root_player[g];
-  compact(p, g, s_child, map);
+  compact(p, g, s_child, map, p.g.half[g], p.g.n_nodes[g]);
   if (threadIdx.x == 0) {
     p.g.root_player[g] = -player;
     p.g.sims_done[g] = 0;
@@ -1473,7 +1567,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(Params p, const int
     __syncthreads();
     if (s_child >= 0) {
       const int player = p.g.root_player[g];
-      compact(p, g, s_child, map);
+      compact(p, g, s_child, map, p.g.half[g], p.g.n_nodes[g]);
       if (threadIdx.x == 0) {
         p.g.root_player[g] = -player;
         p.g.sims_done[g] = 0;
@@ -1504,6 +1598,7 @@ struct az_engine {
   double* d_vroot = nullptr;
   uint64_t* d_own = nullptr;
   uint64_t* d_opp = nullptr;
+  float* d_zero_eval = nullptr;  // rollout mode: zeroed [G*K, 66] stand-in priors / values
   size_t lds_move = 0;
 };
 
@@ -1655,6 +1750,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &e->d_vroot, G));
   chk(dalloc(e, &e->d_own, G));
   chk(dalloc(e, &e->d_opp, G));
+  chk(dalloc(e, &e->d_zero_eval, GK * 66));
   if (rc != AZ_OK) {
     free_all(e);
     delete e;
@@ -1684,7 +1780,8 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
                      p.g.start_step, p.g.noise_cur, p.g.u_cur})
     zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
   zero_ok = zero_ok && hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
-            hipMemset(p.g.sym, 0, GK) == hipSuccess;
+            hipMemset(p.g.sym, 0, GK) == hipSuccess &&
+            hipMemset(e->d_zero_eval, 0, GK * 66 * sizeof(float)) == hipSuccess;
   if (!zero_ok) {
     free_all(e);
     delete e;
@@ -1770,6 +1867,10 @@ int az_expand_backup(az_engine* e, const float* priors, const float* values, voi
   AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
              "az_expand_backup: priors/values required in external-eval mode");
   hipStream_t s = azc::as_stream(stream);
+  if (!priors || !values) {  // rollout mode: k_expand loads rows unconditionally
+    priors = e->d_zero_eval;
+    values = e->d_zero_eval + (size_t)e->p.G * e->p.K * 65;
+  }
   if (e->p.K == 1)
     hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
                        values);
