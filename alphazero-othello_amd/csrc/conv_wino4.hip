@@ -96,7 +96,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-template <int MODE_, int NRT_>
+template <int MODE_, int NRT_, int BOARDS_ = 4>
 struct W4 {
   static constexpr int C = 128, MODE = MODE_;
   static constexpr int PLANES =
@@ -105,8 +105,11 @@ struct W4 {
   // NRT = MFMA row tiles per wave: 2 -> 4 waves (one per SIMD), each weight fragment feeds
   // both row tiles of its wave; 1 -> 8 waves (two per SIMD), row-tile partners request
   // the same fragments
-  static constexpr int NRT = NRT_, WAVES = 8 / NRT, TPT = NRT;
-  static constexpr int BOARDS = 4, ROWS = 64, THREADS = 64 * WAVES;
+  // BOARDS = 4: 64 tiles = two row tiles, 8 / NRT waves, one workgroup per CU (LDS);
+  // BOARDS = 2: one row tile, 4 waves, two workgroups per CU (independent barriers)
+  static constexpr int BOARDS = BOARDS_, ROWS = 16 * BOARDS;
+  static constexpr int NRT = NRT_, WAVES = (ROWS / 32) * 4 / NRT, TPT = NRT;
+  static constexpr int THREADS = 64 * WAVES;
   static constexpr int SLAB = ROWS * 32;            // one (point, plane): 64 tiles x 16 ch x 2 B
   static constexpr int BUF = 4 * PLANES * SLAB;     // one (group, chunk): its four points
   // input chunk slice staged in LDS, zero-padded to 10 x 10 positions per board so a
@@ -733,7 +736,12 @@ extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float*
   // AZ_W4_NRT (experiments): 1 = eight waves of one row tile (default: two waves per SIMD,
   // no AGPR traffic in the fold; bench 79.7 vs 73.5 games/s same-box), 2 = four waves of two
   static const int nrt = getenv("AZ_W4_NRT") ? atoi(getenv("AZ_W4_NRT")) : 1;
+  // AZ_W4_BOARDS (experiments): 2 = two-board workgroups, two per CU
+  static const int nbw = getenv("AZ_W4_BOARDS") ? atoi(getenv("AZ_W4_BOARDS")) : 4;
 #define W4_GO(M, N) launch_wino4<W4<M, N>>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, s)
+  if (mode == AZ_CONV_FP16X2 && nbw == 2)
+    return launch_wino4<W4<AZ_CONV_FP16X2, 1, 2>>(x, wq, bias, res, y, n_boards, relu, in_absmax,
+                                                  out_absmax, s);
   if (mode == AZ_CONV_SPLIT3) return nrt == 1 ? W4_GO(AZ_CONV_SPLIT3, 1) : W4_GO(AZ_CONV_SPLIT3, 2);
   if (mode == AZ_CONV_FP16) return nrt == 1 ? W4_GO(AZ_CONV_FP16, 1) : W4_GO(AZ_CONV_FP16, 2);
   if (mode == AZ_CONV_FP16X2) return nrt == 1 ? W4_GO(AZ_CONV_FP16X2, 1) : W4_GO(AZ_CONV_FP16X2, 2);

@@ -43,6 +43,48 @@ constexpr int kMoveBlock = 256;
 constexpr int kMaxPath = 64;     // one wave lane per path depth for the parallel backup
 constexpr int kMaxLeaves = 8;    // leaves_per_step limit (virtual-loss descents per step)
 
+#ifndef AZ_ENG_STAMP
+#define AZ_ENG_STAMP 0
+#endif
+#if AZ_ENG_STAMP
+// experiment builds only (scripts/build_variants.py -DAZ_ENG_STAMP=1): per-phase
+// s_memrealtime stamps of k_move / k_expand workgroups, records of 8 in a ring no product
+// kernel reads; scripts/eng_stamps.py summarises them
+constexpr int kStampRecs = 1 << 14;
+__device__ unsigned long long g_eng_stamps[kStampRecs * 8];
+__device__ unsigned int g_eng_stamp_n;
+#define ENG_STAMP_BEGIN(kind)                                                    \
+  unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};                          \
+  st_[0] = (kind);                                                               \
+  st_[1] = __builtin_amdgcn_s_memrealtime()
+#define ENG_STAMP(i) st_[i] = __builtin_amdgcn_s_memrealtime()
+__shared__ unsigned long long g_cst[4];  // compact()'s phase stamps (thread 0)
+#define CST(i)                                                  \
+  do {                                                          \
+    if (threadIdx.x == 0) g_cst[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define ENG_STAMP_END()                                                          \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0) {                                               \
+      const unsigned r_ = atomicAdd(&g_eng_stamp_n, 1u) & (kStampRecs - 1);      \
+      for (int i_ = 0; i_ < 8; ++i_) g_eng_stamps[r_ * 8 + i_] = st_[i_];        \
+    }                                                                            \
+  } while (0)
+#else
+#define ENG_STAMP_BEGIN(kind) \
+  do {                        \
+  } while (0)
+#define ENG_STAMP(i) \
+  do {               \
+  } while (0)
+#define ENG_STAMP_END() \
+  do {                  \
+  } while (0)
+#define CST(i) \
+  do {         \
+  } while (0)
+#endif
+
 enum : uint8_t { kExpanded = 1, kTerminal = 2, kChildF64 = 4 };
 enum : int32_t { kIdle = AZ_GAME_IDLE, kActive = AZ_GAME_ACTIVE, kFinished = AZ_GAME_FINISHED,
                  kSearchDone = 3 };
@@ -792,6 +834,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < K) in[j] = load_leaf_in(p, row0 + j, priors, values);
+  ENG_STAMP_BEGIN(2);
   // every load above in flight before any is waited for (the compiler would otherwise sink
   // them past the early exit below, one dependent round trip each)
   asm volatile("" ::"v"(half), "v"(n_nodes), "v"(sd0), "v"(target));
@@ -803,6 +846,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) in[j].sym = p.d4 ? in[j].sym : 0;
   if (in[0].leaf < 0) return;
+  ENG_STAMP(2);
   double done_v[KMAX];
   int n_sims = 0;
 #pragma unroll
@@ -837,6 +881,8 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
       else p.g.status[g] = kSearchDone;
     }
   }
+  ENG_STAMP(3);
+  if ((g & 63) == 0) ENG_STAMP_END();
 }
 
 // ---------------------------------------------------------------------------------
@@ -982,6 +1028,7 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
   const int lane = tid & 63, wave = tid >> 6;
   const int nh = oh ^ 1;
   const int span = n_nodes - child;  // candidates: old nodes child .. n_nodes-1
+  CST(0);
   // 1. rel[j] = parent of old node child+j as an offset from `child` (descendants of `child`
   // all lie above it; a parent below it means "not in the subtree")
   for (int j0 = 0; j0 < span; j0 += kMoveBlock * kP) {
@@ -998,6 +1045,7 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
     }
   }
   __syncthreads();
+  CST(1);
   // 2. pointer jumping until every link is 0 (member) or kOut; in-place updates only ever
   // replace a link by one of its ancestors' links.  Each round jumps twice, and a thread
   // keeps kU independent LDS reads in flight (the loop is LDS-latency-bound otherwise).
@@ -1024,6 +1072,7 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
     }
     if (!__syncthreads_or(more)) break;
   }
+  CST(2);
   // 3. new index = rank among members (block exclusive scan over contiguous thread ranges)
   const int per = (span + kMoveBlock - 1) / kMoveBlock;
   const int j0 = tid * per, j1 = min(j0 + per, span);
@@ -1052,6 +1101,7 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
     }
   }
   __syncthreads();
+  CST(3);
   // 4. copy the members, translating parent / first-child links: kC nodes per thread with
   // every load issued before the first store (one global round trip per kC * block nodes
   // instead of one per block of nodes)
@@ -1224,6 +1274,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
   const int tid = threadIdx.x;
   const int n_ready = p.ctr->ready_n;
   for (int ri = blockIdx.x; ri < n_ready; ri += gridDim.x) {
+    ENG_STAMP_BEGIN(1);
     const int g = p.ready[ri];
     const int half = p.g.half[g];
     const int ply = p.g.ply[g];
@@ -1325,6 +1376,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
       }
     }
     __syncthreads();
+    ENG_STAMP(2);
     if (s_term) {
       const int n_plies = ply + 1 < p.T ? ply + 1 : p.T;
       finish_game(p, g, n_plies, s_winner, map);
@@ -1360,8 +1412,13 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
         p.g.sims_done[g] = 0;
         p.g.sims_target[g] = p.sims;
       }
+#if AZ_ENG_STAMP
+      for (int i = 0; i < 4; ++i) st_[3 + i] = g_cst[i];
+#endif
     }
     __syncthreads();
+    ENG_STAMP(7);
+    if (threadIdx.x < 64) ENG_STAMP_END();
   }
   __syncthreads();
   // the last workgroup to finish (every workgroup has read ready_n by then) clears the
@@ -1635,6 +1692,14 @@ unsigned sel_grid(const az_engine* e) {
 }  // namespace
 
 extern "C" {
+
+#if AZ_ENG_STAMP
+int az_eng_stamps(unsigned long long* host, unsigned* n_written) {
+  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_eng_stamps), sizeof(g_eng_stamps)));
+  AZ_HIP(hipMemcpyFromSymbol(n_written, HIP_SYMBOL(g_eng_stamp_n), sizeof(unsigned)));
+  return AZ_OK;
+}
+#endif
 
 int az_engine_create(const az_config* cfg_in, az_engine** out) {
   AZ_GUARD_BEGIN

@@ -1,0 +1,63 @@
+"""Per-phase latency of the engine kernels at steady state, from an AZ_ENG_STAMP build
+(scripts/build_variants.py stamp "-DAZ_ENG_STAMP=1", loaded through AZ_LIB_PATH):
+k_move per ready game (root/children load + pi + sample; compaction: parent loads, pointer
+jumping, scan, copy; end) and k_expand per sampled slot (first round trip, the rest), in
+microseconds (s_memrealtime, 100 MHz): medians / 90th percentiles over the last records.
+
+    AZ_LIB_PATH=... python scripts/eng_stamps.py [warm_steps] > out.json"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "alphazero-othello_amd")]
+import az_native as nat  # noqa: E402
+import bench  # noqa: E402
+from engine import BatchedSelfPlay  # noqa: E402
+from Models import AlphaZeroNet  # noqa: E402
+
+
+def stats(x):
+    x = np.asarray(x, np.float64) / 100.0  # 100 MHz ticks -> us
+    return {"n": int(len(x)), "p50": round(float(np.median(x)), 2),
+            "p90": round(float(np.percentile(x, 90)), 2), "mean": round(float(x.mean()), 2)}
+
+
+def main():
+    warm = int(sys.argv[1]) if len(sys.argv) > 1 else 26000
+    torch.manual_seed(0)
+    sp = BatchedSelfPlay(AlphaZeroNet(8, 65, 5, 128), bench.SELFPLAY_ARGS, 1024, seed=1,
+                         precision="fp16x2")
+    sp.reset(-1, 401 * 60)
+    for _ in range(warm // 2000):
+        sp.step(2000)
+        torch.cuda.synchronize()
+        print("warm", file=sys.stderr, flush=True)
+    sp.step(400)
+    torch.cuda.synchronize()
+    recs = (ctypes.c_ulonglong * (16384 * 8))()
+    n = ctypes.c_uint()
+    nat.lib.az_eng_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    nat.check(nat.lib.az_eng_stamps(ctypes.addressof(recs), ctypes.byref(n)), "az_eng_stamps")
+    a = np.frombuffer(recs, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    a = a[a[:, 1] > 0]
+    mv, ex = a[a[:, 0] == 1], a[a[:, 0] == 2]
+    cmp_ = mv[mv[:, 3] > 0]
+    out = {"records": int(n.value),
+           "k_move": {"total": stats(mv[:, 7] - mv[:, 1]), "root_pi_sample": stats(mv[:, 2] - mv[:, 1]),
+                      "compact_parents": stats(cmp_[:, 4] - cmp_[:, 3]),
+                      "compact_jumping": stats(cmp_[:, 5] - cmp_[:, 4]),
+                      "compact_scan": stats(cmp_[:, 6] - cmp_[:, 5]),
+                      "compact_copy": stats(cmp_[:, 7] - cmp_[:, 6]),
+                      "game_end_total": stats((mv[mv[:, 3] == 0][:, 7] - mv[mv[:, 3] == 0][:, 1]))},
+           "k_expand": {"total": stats(ex[:, 3] - ex[:, 1]), "first_round_trip": stats(ex[:, 2] - ex[:, 1]),
+                        "rest": stats(ex[:, 3] - ex[:, 2])}}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
