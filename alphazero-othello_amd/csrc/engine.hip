@@ -504,6 +504,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   const int64_t row0 = (int64_t)g * K;
   const int lane = lane_id();
   // every per-slot word in one round trip
+  ENG_STAMP_BEGIN(3);
   const int status = p.g.status[g];
   const unsigned long long step = p.ctr->step;
   const int start_step = p.g.start_step[g];
@@ -608,6 +609,12 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       atomicAdd(&p.ctr->overflow, 1ull);
     }
   }
+  ENG_STAMP(3);
+#if AZ_ENG_STAMP
+  st_[4] = (unsigned long long)w.n;
+  st_[5] = (unsigned long long)sims_done;
+#endif
+  ENG_STAMP_END();
 }
 
 // ---------------------------------------------------------------------------------
@@ -882,7 +889,13 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
     }
   }
   ENG_STAMP(3);
-  if ((g & 63) == 0) ENG_STAMP_END();
+#if AZ_ENG_STAMP
+  st_[4] = (unsigned long long)in[0].leaf;
+  st_[5] = (unsigned long long)in[0].plen;
+  st_[6] = (unsigned long long)n_nodes;
+  st_[7] = (unsigned long long)g;
+#endif
+  ENG_STAMP_END();
 }
 
 // ---------------------------------------------------------------------------------

@@ -23,6 +23,8 @@ from Models import AlphaZeroNet  # noqa: E402
 
 def stats(x):
     x = np.asarray(x, np.float64) / 100.0  # 100 MHz ticks -> us
+    if not len(x):
+        return {"n": 0}
     return {"n": int(len(x)), "p50": round(float(np.median(x)), 2),
             "p90": round(float(np.percentile(x, 90)), 2), "mean": round(float(x.mean()), 2)}
 
@@ -56,6 +58,32 @@ def main():
                       "game_end_total": stats((mv[mv[:, 3] == 0][:, 7] - mv[mv[:, 3] == 0][:, 1]))},
            "k_expand": {"total": stats(ex[:, 3] - ex[:, 1]), "first_round_trip": stats(ex[:, 2] - ex[:, 1]),
                         "rest": stats(ex[:, 3] - ex[:, 2])}}
+    # per launch: waves of one launch start within a few us of each other; launches are
+    # separated by the rest of the step (>= 400 us): split on gaps in the start stamps
+    for kind, name in ((2, "k_expand"), (3, "k_select")):
+        r = a[a[:, 0] == kind]
+        r = r[np.argsort(r[:, 1])]
+        if not len(r):
+            continue
+        cut = np.flatnonzero(np.diff(r[:, 1]) > 10000) + 1  # 100 us
+        spans, starts, ends = [], [], []
+        for grp in np.split(r, cut):
+            if len(grp) < 256:
+                continue
+            spans.append(grp[:, 3].max() - grp[:, 1].min())
+            starts.append(np.percentile(grp[:, 1] - grp[:, 1].min(), 90))
+            ends.append(np.percentile(grp[:, 3] - grp[:, 1].min(), 50))
+        out.setdefault(name, {})
+        out[name]["launch_span_first_start_to_last_end"] = stats(spans)
+        out[name]["launch_p90_wave_start_offset"] = stats(starts)
+        out[name]["launch_median_wave_end_offset"] = stats(ends)
+        if kind == 3:
+            out[name]["wave_total"] = stats(r[:, 3] - r[:, 1])
+    # the slowest k_expand waves: leaf (0 = a root expansion), path length, arena size, slot
+    ex = ex[np.argsort(ex[:, 3] - ex[:, 1])]
+    out["k_expand_slowest"] = [{"us": round((r[3] - r[1]) / 100.0, 2), "leaf": int(r[4]),
+                                "plen": int(r[5]), "n_nodes": int(r[6]), "slot": int(r[7])}
+                               for r in ex[-12:]]
     print(json.dumps(out, indent=1))
 
 
