@@ -1006,17 +1006,26 @@ __device__ float root_pi_pre(int nc, uint64_t lg, int cnt_lane, double temp, dou
 }
 
 // np.random.choice(65, p=pi) given its uniform draw u: cdf = cumsum(float64(pi)) (sequential),
-// cdf /= cdf[-1], searchsorted(u, side='right').  Lane 0 only; the second pass recomputes
-// the same sequential partial sums instead of keeping a 65-entry array in scratch.
-__device__ int sample_action(const float* pis, double u) {
-  double last = 0.0;
-  for (int a = 0; a < 65; ++a) last = last + (double)pis[a];
-  double acc = 0.0;
-  int idx = 0;
-  for (int a = 0; a < 65; ++a) {
-    acc = acc + (double)pis[a];
-    if (acc / last <= u) idx = a + 1;
+// cdf /= cdf[-1], searchsorted(u, side='right').  Whole wave: lane 0 forms the sequential
+// partial sums (NumPy's cumsum order) into `cdf` (LDS, 65 doubles), then every lane divides
+// and compares its own entry at once -- the cdf is non-decreasing (pi >= 0) and the
+// correctly rounded division is monotone, so the entries <= u are a prefix and the answer is
+// their count (all-zero pi: 0/0 compares false everywhere, as in NumPy's loop).
+__device__ int sample_action(const float* pis, double u, double* cdf) {
+  const int lane = lane_id();
+  if (lane == 0) {
+    double acc = 0.0;
+    for (int a = 0; a < 65; ++a) {
+      acc = acc + (double)pis[a];
+      cdf[a] = acc;
+    }
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  const double last = cdf[64];
+  const bool le = cdf[lane] / last <= u;
+  const bool le64 = cdf[64] / last <= u;
+  const int idx = azb::popc(ballot(le)) + (le64 ? 1 : 0);
   return idx > 64 ? 64 : idx;
 }
 
@@ -1086,11 +1095,18 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
     if (!__syncthreads_or(more)) break;
   }
   CST(2);
-  // 3. new index = rank among members (block exclusive scan over contiguous thread ranges)
-  const int per = (span + kMoveBlock - 1) / kMoveBlock;
+  // 3. new index = rank among members (block exclusive scan over contiguous thread ranges of
+  // a multiple of 8 links, read 16 bytes at a time; entries past `span` are masked)
+  const int per = (((span + kMoveBlock - 1) / kMoveBlock) + 7) & ~7;
   const int j0 = tid * per, j1 = min(j0 + per, span);
   int cnt = 0;
-  for (int j = j0; j < j1; ++j) cnt += rel[j] == 0;
+  for (int j = j0; j < j1; j += 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rel + j);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      cnt += (j + k < j1 && ((w[k >> 1] >> (16 * (k & 1))) & 0xffffu) == 0) ? 1 : 0;
+  }
   int incl = cnt;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1105,12 +1121,28 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
     n_new += s_scan[w];
   }
   int r = base + incl - cnt;
-  for (int j = j0; j < j1; ++j) {
-    if (rel[j] == 0) {
-      inv[r] = (uint16_t)j;
-      rel[j] = (uint16_t)r++;
+  for (int j = j0; j < j1; j += 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rel + j);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool member = ((w[k >> 1] >> (16 * (k & 1))) & 0xffffu) == 0;
+      uint32_t nv = kOut;
+      if (j + k < j1 && member) {
+        inv[r] = (uint16_t)(j + k);
+        nv = (uint32_t)r++;
+      }
+      o[k >> 1] |= (nv & 0xffffu) << (16 * (k & 1));
+    }
+    // whole 16-byte group written back: links past j1 belong to the next thread's range
+    // (or lie past `span`), so only the valid ones are stored
+    if (j + 8 <= j1) {
+      *reinterpret_cast<uint4*>(rel + j) = make_uint4(o[0], o[1], o[2], o[3]);
     } else {
-      rel[j] = kOut;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (j + k < j1) rel[j + k] = (uint16_t)((o[k >> 1] >> (16 * (k & 1))) & 0xffffu);
     }
   }
   __syncthreads();
@@ -1281,8 +1313,9 @@ __device__ void finish_game(const Params& p, int g, int n_plies, int winner, int
 
 // k_move: one workgroup per slot in the ready list.
 __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
-  extern __shared__ int32_t map[];
+  extern __shared__ __align__(16) int32_t map[];
   __shared__ float s_pi[65];
+  __shared__ double s_cdf[65];
   __shared__ int s_child, s_term, s_winner, s_restart;
   const int tid = threadIdx.x;
   const int n_ready = p.ctr->ready_n;
@@ -1338,7 +1371,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
         if (injected) p.g.u_cur[g] = (int)(rng0 + used);
         else p.g.rng_event[g] = rng0 + used;
       }
-      u_tie = shfl(u_tie, 0);
+      u_tie = readlane(u_tie, 0);
       // ---- pi (MCTS_model.py:244-271) and trajectory record (self_play_worker.py:72-73)
       float p64;
       const float pi = root_pi_pre(nc, lg, c_n, temp, u_tie, &p64);
@@ -1351,6 +1384,7 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
       // ---- action sample (self_play_worker.py:75) and the chosen child (MCTS.make_move,
       // MCTS_model.py:200-215): the children are every legal action in ascending order (or
       // the single pass), so the child's index follows from the root's legal mask
+      const int a = sample_action(s_pi, readlane(u_act, 0), s_cdf);
       int jc = -1;
       if (tid == 0) {
         if (room) {
@@ -1360,7 +1394,6 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
           p.g.t_player[(int64_t)g * p.T + ply] = (int8_t)player;
           p.g.t_vroot[(int64_t)g * p.T + ply] = r_n == 0 ? 0.0 : r_w / (double)r_n;
         }
-        const int a = sample_action(s_pi, u_act);
         if (nc > 0) {
           if (lg) {
             if (a < 64 && ((lg >> a) & 1)) jc = azb::popc(lg & ((1ull << a) - 1ull));
@@ -1369,10 +1402,10 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
           }
         }
       }
-      jc = shfl(jc, 0);
+      jc = readlane(jc, 0);
       const int src = jc >= 0 ? jc : 0;
-      const int ch_flags = shfl(c_flags, src);
-      const uint64_t ch_own = shfl(c_own, src), ch_opp = shfl(c_opp, src);
+      const int ch_flags = readlane(c_flags, src);
+      const uint64_t ch_own = readlane(c_own, src), ch_opp = readlane(c_opp, src);
       if (tid == 0) {
         s_child = jc >= 0 ? fc + jc : -1;
         int term = 1, winner = 0;
@@ -1536,7 +1569,7 @@ __global__ void k_policy(Params p, int slot, double temp, double u_tie, float* p
 
 __global__ __launch_bounds__(kMoveBlock) void k_reroot(Params p, int g, int action,
                                                        int32_t* result) {
-  extern __shared__ int32_t map[];
+  extern __shared__ __align__(16) int32_t map[];
   __shared__ int s_child;
   const int half = p.g.half[g];
   if (threadIdx.x == 0) {
@@ -1616,7 +1649,7 @@ __global__ __launch_bounds__(kSelBlock) void k_root_stats(Params p, int32_t* cou
 // found[g] = child node or -1 (KeyError / no tree); one workgroup per slot
 __global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(Params p, const int32_t* actions,
                                                              int32_t* found) {
-  extern __shared__ int32_t map[];
+  extern __shared__ __align__(16) int32_t map[];
   __shared__ int s_child;
   for (int g = blockIdx.x; g < p.G; g += gridDim.x) {
     const int action = actions[g];
