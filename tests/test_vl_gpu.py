@@ -177,3 +177,76 @@ def test_virtual_loss_self_play_matches_oracle():
 def test_leaves_per_step_bounds():
     with pytest.raises(RuntimeError, match="leaves_per_step"):
         Engine(1, 4, auto_play=False, leaves_per_step=9)
+
+
+def test_virtual_loss_with_fused_d4_and_equivariant_policy_is_invisible():
+    """K = 4 leaves per step with the fused per-leaf D4 transform (config #5): a D4-equivariant
+    policy must give the same searches with and without it (each row's own transform is
+    inverted on its own priors)."""
+    import torch
+
+    def eq_eval(planes):
+        pr = torch.cat([planes * 0.25 + 1.0, torch.ones_like(planes[:, :1])], 1)
+        return pr.contiguous(), (planes.sum(1) / 64.0).contiguous()
+
+    res = []
+    for d4 in (False, True):
+        e = Engine(4, 60, d4_augment=d4, auto_play=False, seed=5, leaves_per_step=4)
+        for s in range(4):
+            e.set_root(s, 0x0000000810000000, 0x0000001008000000, 1)
+        e.begin_search(-1, 60)
+        for _ in range(500):
+            e.select()
+            pr, va = eq_eval(e.nn_in)
+            e.priors.copy_(pr)
+            e.values.copy_(va)
+            e.expand()
+            e.play()
+            if (e.game_info()["status"] != nat.AZ_GAME_ACTIVE).all():
+                break
+        res.append([e.root_policy(s, 1.0)[1] for s in range(4)])
+    for a, b in zip(*res):
+        assert (a == b).all() and a.sum() == 60
+
+
+def test_virtual_loss_rollout_mode_counts():
+    """Rollout evaluation (policy None) with K = 4: every search completes its simulations."""
+    e = Engine(8, 32, rollout=True, auto_play=False, leaves_per_step=4)
+    for s in range(8):
+        e.set_root(s, 0x0000000810000000, 0x0000001008000000, 1)
+    e.begin_search(-1, 32)
+    for _ in range(200):
+        e.select()
+        e.expand(e.priors, e.values)
+        e.play()
+        if (e.game_info()["status"] != nat.AZ_GAME_ACTIVE).all():
+            break
+    for s in range(8):
+        _, counts, _ = e.root_policy(s, 1.0)
+        assert counts.sum() == 32
+    assert e.counters()["arena_overflows"] == 0
+
+
+def test_batched_selfplay_with_virtual_loss_properties():
+    """BatchedSelfPlay with a random-init net, device RNG and K = 4 leaves per game per step:
+    every finished game yields well-formed training tuples."""
+    import torch
+
+    from engine import BatchedSelfPlay
+    from Models import FastOthelloNet
+
+    torch.manual_seed(0)
+    args = {"c_puct": 2.0, "num_simulations": 16, "dirichlet_alpha": 1.0,
+            "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
+            "lambda": 0.98}
+    sp = BatchedSelfPlay(FastOthelloNet(8, 65), args, 32, seed=1, use_graph=True,
+                         leaves_per_step=4)
+    assert sp.engine.nn_in.shape == (128, 64)
+    tuples = sp.play_games(48)
+    c = sp.engine.counters()
+    assert c["games_finished"] == 48 and c["arena_overflows"] == 0
+    smp = sp.engine.samples()
+    assert len(tuples) == c["samples"] >= 9 * 48
+    assert ((smp["own"] & smp["opp"]) == 0).all()
+    assert np.allclose(smp["pi"].sum(1), 1.0, atol=1e-5)
+    assert (np.abs(smp["z"]) <= 1.0).all()
