@@ -67,6 +67,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
   const float4* hp = reinterpret_cast<const float4*>(h + ((size_t)(live ? b : 0) * 64 + lane) * C);
 #pragma unroll
   for (int c = 0; c < C / 4; ++c) x[c] = hp[c];
+  // the lane's policy-FC weights (L2) in the same round trip as its activation row
+  float wpl[128];
+  float wl0 = 0.f, wl1 = 0.f;
+  if (!STAGE) {
+#pragma unroll
+    for (int k = 0; k < 128; ++k) wpl[k] = wpolT[k * 65 + lane];
+    wl0 = wpolT[lane * 65 + 64];
+    wl1 = wpolT[(lane + 64) * 65 + 64];
+  }
   if (STAGE) {
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
@@ -95,11 +104,24 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
   __syncthreads();
   if (!live) return;  // whole wave (b is uniform per wave); no barrier follows
 
-  // policy FC: lane a -> logit a; logit 64 split over the lanes and reduced
+  // policy FC: lane a -> logit a; logit 64 split over the lanes and reduced.  The FC weights
+  // come from L2 (shared by every workgroup): a lane's 128 policy weights were requested with
+  // its activation row, its 64 value-weight quads are requested here before any FMA (one round
+  // trip each instead of one per 16-iteration batch; one wave per SIMD, so the registers are
+  // there)
+  float4 wq[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) wq[i] = reinterpret_cast<const float4*>(w1s + i * 256)[lane];
+  if (STAGE) {
+#pragma unroll
+    for (int k = 0; k < 128; ++k) wpl[k] = wpol[k * 65 + lane];
+    wl0 = wpol[lane * 65 + 64];
+    wl1 = wpol[(lane + 64) * 65 + 64];
+  }
   float la = bpol[lane];
-#pragma unroll 16
-  for (int k = 0; k < 128; ++k) la += wpol[k * 65 + lane] * s_p[w][k];
-  float l64 = wpol[lane * 65 + 64] * s_p[w][lane] + wpol[(lane + 64) * 65 + 64] * s_p[w][lane + 64];
+#pragma unroll
+  for (int k = 0; k < 128; ++k) la += wpl[k] * s_p[w][k];
+  float l64 = wl0 * s_p[w][lane] + wl1 * s_p[w][lane + 64];
   l64 = wave_sum(l64) + bpol[64];
   const float m = fmaxf(wave_max(la), l64);
   const float e = __expf(la - m), e64 = __expf(l64 - m);
@@ -109,14 +131,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_heads_az(
 
   // value: lane j -> hidden units 4j..4j+3 of val_fc1, then val_fc2 reduced over the wave
   float4 acc = reinterpret_cast<const float4*>(b1)[lane];
-#pragma unroll 16
+#pragma unroll
   for (int i = 0; i < 64; ++i) {
-    const float4 wq = reinterpret_cast<const float4*>(w1s + i * 256)[lane];
     const float vi = s_v[w][i];
-    acc.x += wq.x * vi;
-    acc.y += wq.y * vi;
-    acc.z += wq.z * vi;
-    acc.w += wq.w * vi;
+    acc.x += wq[i].x * vi;
+    acc.y += wq[i].y * vi;
+    acc.z += wq[i].z * vi;
+    acc.w += wq[i].w * vi;
   }
   const float4 o = reinterpret_cast<const float4*>(w2)[lane];
   const float part = fmaxf(acc.x, 0.f) * o.x + fmaxf(acc.y, 0.f) * o.y +
