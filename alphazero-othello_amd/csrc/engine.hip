@@ -111,6 +111,8 @@ struct Games {
   int32_t* n_nodes;
   int32_t* sims_done;
   int32_t* sims_target;
+  unsigned long long* sims_acc;  // simulations completed by the slot (summed into ctr->sims
+                                 // by az_counters: no device-wide atomic per wave per step)
   int32_t* leaf;       // [G, K] leaves awaiting evaluation in descent order, -1 ends the list
   int32_t* path;       // [G, K, kMaxPath] root..leaf node indices of each pending leaf
   int32_t* path_len;   // [G, K] entries in `path`; 0 => deeper than kMaxPath, walk parents
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   if (lane == 0) {
     const int prev = p.g.sims_done[g];
     if (sims_done != prev) {
-      atomicAdd(&p.ctr->sims, (unsigned long long)(sims_done - prev));
+      p.g.sims_acc[g] += (unsigned long long)(sims_done - prev);
       p.g.sims_done[g] = sims_done;
     }
     if (w.n == 0 && sims_done >= target) {
@@ -881,7 +883,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
     const int sd = sd0 + n_sims;
     if (n_sims) {
       p.g.sims_done[g] = sd;
-      atomicAdd(&p.ctr->sims, (unsigned long long)n_sims);
+      p.g.sims_acc[g] += (unsigned long long)n_sims;
     }
     if (sd >= target) {
       if (p.auto_play) push_ready(p, g);
@@ -1480,6 +1482,22 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
   }
 }
 
+// ctr->sims = sum of the slots' counters (one workgroup; az_counters only)
+__global__ __launch_bounds__(1024) void k_sum_sims(Params p) {
+  __shared__ unsigned long long s_part[1024 / kWave];
+  unsigned long long v = 0;
+  for (int g = threadIdx.x; g < p.G; g += blockDim.x) v += p.g.sims_acc[g];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t += s_part[w];
+    p.ctr->sims = t;
+  }
+}
+
 // step counter for engines without auto-play (k_move not launched)
 __global__ void k_tick(Counters* c) { c->step += 1; }
 
@@ -1503,6 +1521,7 @@ __global__ void k_reset(Params p, long long budget, int stagger) {
   if (g >= p.G) return;
   p.g.half[g] = 0;
   p.g.overflow[g] = 0;
+  p.g.sims_acc[g] = 0;
   p.g.rng_event[g] = 0;
   p.g.noise_cur[g] = 0;
   p.g.u_cur[g] = 0;
@@ -1817,6 +1836,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.g.n_nodes, G));
   chk(dalloc(e, &p.g.sims_done, G));
   chk(dalloc(e, &p.g.sims_target, G));
+  chk(dalloc(e, &p.g.sims_acc, G));
   const size_t GK = G * (size_t)p.K;
   chk(dalloc(e, &p.g.leaf, GK));
   chk(dalloc(e, &p.g.path, GK * kMaxPath));
@@ -1890,7 +1910,8 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
                      p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
                      p.g.start_step, p.g.noise_cur, p.g.u_cur})
     zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
-  zero_ok = zero_ok && hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
+  zero_ok = zero_ok && hipMemset(p.g.sims_acc, 0, G * sizeof(unsigned long long)) == hipSuccess &&
+            hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
             hipMemset(p.g.sym, 0, GK) == hipSuccess &&
             hipMemset(e->d_zero_eval, 0, GK * 66 * sizeof(float)) == hipSuccess;
   if (!zero_ok) {
@@ -2000,7 +2021,10 @@ int az_play(az_engine* e, void* stream) {
     AZ_HIP(hipGetLastError());
     return AZ_OK;
   }
-  const int blocks = e->p.G < 256 ? e->p.G : 256;
+  // the ready list holds a few slots per step (G / (sims + 1) / plies on average): 64
+  // workgroups take them grid-stride, and each workgroup's closing atomic on the shared
+  // move_done counter stays cheap (one address serialises ~90 atomics per microsecond)
+  const int blocks = e->p.G < 64 ? e->p.G : 64;
   hipLaunchKernelGGL(k_move, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->p);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -2130,6 +2154,8 @@ int az_reroot_slots(az_engine* e, const int32_t* actions, int32_t* found, void* 
 int az_counters(az_engine* e, int64_t* out8, void* stream) {
   AZ_REQUIRE(e && out8, AZ_ERR_ARG, "null argument");
   hipStream_t s = azc::as_stream(stream);
+  hipLaunchKernelGGL(k_sum_sims, dim3(1), dim3(1024), 0, s, e->p);
+  AZ_HIP(hipGetLastError());
   Counters c;
   AZ_HIP(hipMemcpyAsync(&c, e->p.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
   AZ_HIP(hipStreamSynchronize(s));
