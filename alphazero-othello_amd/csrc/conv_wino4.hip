@@ -65,6 +65,11 @@
 #ifndef AZ_W4_SCHED
 #define AZ_W4_SCHED 0
 #endif
+// wave priority (experiments): 1 = s_setprio 1 once for the younger half of an 8-wave
+// workgroup (waves 4-7), 2 = s_setprio 1 / 0 around each step's MFMA cluster
+#ifndef AZ_W4_PRIO
+#define AZ_W4_PRIO 0
+#endif
 // timing proxy of a two-plane split (wrong numerics): 2 planes, 3 products
 #ifndef AZ_W4_PROXY2
 #define AZ_W4_PROXY2 0
@@ -413,8 +418,10 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
     }
     const int slot = (4 * PAR + l) % G::RING;  // = step % RING (folds: l is unrolled)
     if (!(AZ_W4_EXP & 4)) {
+      if (AZ_W4_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int t = 0; t < G::NRT; ++t) mma<G>(S.acc[l][t], S.af[t], S.bf[slot]);
+      if (AZ_W4_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
     if (l == 0 && !(AZ_W4_EXP & 2)) {
       // chunk L+1's window rows (requested right after the previous barrier) combined
@@ -646,6 +653,8 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     }
   }
   W4_STAMP(1);
+  if (AZ_W4_PRIO == 1 && G::WAVES == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+    __builtin_amdgcn_s_setprio(1);
   run_group<G, 0>(S);
   W4_STAMP(2);
   run_group<G, 1>(S);
