@@ -5,7 +5,9 @@ Each net owns one host-driven engine whose slot g is that net's tree in match g 
 reference gives each player its own `MCTS` with tree reuse).  Per ply, every match's side
 to move searches in its own engine (temperature 0, no root noise: eval.py builds its
 trees with the default dirichlet_epsilon = 0); both engines' searches run concurrently,
-one leaf per searching slot per step; the action is the argmax of the root visit counts
+`args['num_threads']` virtual-loss leaves per searching slot per step (the reference's
+worker count, default 4, MCTS_model.py:196); the action is the argmax of the
+root visit counts
 with the reference's random tie break (np.random.choice over the tied maxima,
 MCTS_model.py:250-254); the board advances through the C-ABI step; both trees re-root on
 the action (eval.py:176-177).  Colours alternate by match index as in
@@ -45,7 +47,7 @@ class BatchedArena:
         self.args = args
         self.G = n_slots
         kw = dict(c_puct=args["c_puct"], auto_play=False, node_capacity=node_capacity,
-                  device=device)
+                  device=device, leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
         self.eng = [Engine(n_slots, args["num_simulations"], rollout=net_a is None, seed=seed,
                            **kw),
                     Engine(n_slots, args["num_simulations"], rollout=net_b is None,

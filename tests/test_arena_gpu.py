@@ -28,8 +28,11 @@ def oracle_play_match(first_salt, second_salt, args):
             return p.astype(np.float32), float(v)
         return f
 
-    trees = {1: SeqMCTS(args["c_puct"], args["num_simulations"], ev(first_salt), rng=LowestTie()),
-             -1: SeqMCTS(args["c_puct"], args["num_simulations"], ev(second_salt), rng=LowestTie())}
+    K = args.get("num_threads", 4)  # the reference's default worker count (MCTS_model.py:196)
+    trees = {1: SeqMCTS(args["c_puct"], args["num_simulations"], ev(first_salt), rng=LowestTie(),
+                        leaves_per_step=K),
+             -1: SeqMCTS(args["c_puct"], args["num_simulations"], ev(second_salt), rng=LowestTie(),
+                         leaves_per_step=K)}
     game = ob.OracleGame()
     state, player, plies = game.get_initial_state(), 1, 0
     while True:
@@ -50,8 +53,12 @@ def oracle_play_match(first_salt, second_salt, args):
         player = -player
 
 
-def test_arena_matches_oracle_play_match():
+@pytest.mark.parametrize("threads", [None, 1])
+def test_arena_matches_oracle_play_match(threads):
+    # eval.py's args carry no num_threads: the reference's default of 4 workers
     args = {"c_puct": 2.0, "num_simulations": 16}
+    if threads is not None:
+        args["num_threads"] = threads
     arena = BatchedArena(lambda x: mock_eval_torch(x, 1), lambda x: mock_eval_torch(x, 2), args,
                          n_slots=4, tie_break=tie_break_lowest)
     wa, wb, dr, plies = arena.play(4)
