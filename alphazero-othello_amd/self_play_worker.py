@@ -69,12 +69,15 @@ def one_self_play(args_tuple):
 def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, stream_id=0,
                             d4_augment=False, dtype=torch.float32):
     """Batched replacement of Trainer.collect_self_play_games' pool (train.py:199-225):
-    `num_games` games on one GPU, `n_slots` at a time (default min(num_games, 4096)).
-    Returns the concatenated training tuples of all games."""
+    `num_games` games on one GPU, `n_slots` at a time (default min(num_games, 4096)), each
+    searching with args['num_threads'] virtual-loss leaves per step (the reference's worker
+    count, default 4: MCTS_model.py:196).  Returns the concatenated training tuples of all
+    games."""
     from engine import BatchedSelfPlay
 
     n_slots = n_slots or min(num_games, 4096)
     sp = BatchedSelfPlay(policy, args, n_slots, seed=seed, stream_id=stream_id,
                          d4_augment=d4_augment, dtype=dtype,
-                         sample_capacity=num_games * 130)
+                         sample_capacity=num_games * 130,
+                         leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
     return sp.play_games(num_games)

@@ -250,3 +250,27 @@ def test_batched_selfplay_with_virtual_loss_properties():
     assert ((smp["own"] & smp["opp"]) == 0).all()
     assert np.allclose(smp["pi"].sum(1), 1.0, atol=1e-5)
     assert (np.abs(smp["z"]) <= 1.0).all()
+
+
+@pytest.mark.parametrize("threads", [None, 1])
+def test_collect_self_play_games_drop_in(threads):
+    """self_play_worker.collect_self_play_games (the batched replacement of train.py's pool)
+    at the reference's default worker count (4 leaves per step) and at num_threads = 1:
+    the reference's training tuples, one list per call."""
+    import torch
+
+    from Models import FastOthelloNet
+    from self_play_worker import collect_self_play_games
+
+    torch.manual_seed(0)
+    args = {"c_puct": 2.0, "num_simulations": 12, "dirichlet_alpha": 1.0,
+            "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
+            "lambda": 0.98}
+    if threads is not None:
+        args["num_threads"] = threads
+    out = collect_self_play_games(FastOthelloNet(8, 65), args, 20)
+    assert len(out) >= 9 * 20
+    for s, pi, z in out:
+        assert s.shape == (8, 8) and s.dtype == np.int8
+        assert pi.shape == (65,) and abs(float(pi.sum()) - 1.0) < 1e-5
+        assert -1.0 <= z <= 1.0
