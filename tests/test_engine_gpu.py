@@ -127,6 +127,8 @@ def test_selfplay_games_match_reference_on_device():
         c = e.counters()
         assert c["games_finished"] == G and c["arena_overflows"] == 0
         smp = e.samples()
+        # every move is exactly S simulations (per-slot counts summed by az_counters)
+        assert c["simulations"] == S * len(smp["z"]) and c["moves"] == len(smp["z"])
         for s, g in enumerate(games):
             sel = d["game"] == g
             mine = smp["slot"] == s

@@ -224,7 +224,9 @@ def test_virtual_loss_rollout_mode_counts():
     for s in range(8):
         _, counts, _ = e.root_policy(s, 1.0)
         assert counts.sum() == 32
-    assert e.counters()["arena_overflows"] == 0
+    c = e.counters()
+    assert c["arena_overflows"] == 0
+    assert c["simulations"] == 8 * 32  # per-slot counts summed by az_counters
 
 
 def test_batched_selfplay_with_virtual_loss_properties():
