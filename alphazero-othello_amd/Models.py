@@ -159,7 +159,7 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
     With `fused` (AlphaZeroNet / FastOthelloNet) the convolutions run without bias and one
     HIP epilogue applies bias + residual + ReLU.  conv="hip" runs the 3x3 trunk on the
     fused MFMA kernels, in `precision`:
-      "split3" (default for fp32): bf16x3-split operands on the 16-bit MFMA pipe, six
+      "split3": bf16x3-split operands on the 16-bit MFMA pipe, six
                partial products accumulated in fp32 — fp32-accurate (csrc/conv16.hip, or
                at 128 channels the Winograd F(2x2,3x3) form csrc/conv_wino.hip;
                tests/test_nn_gpu.py bounds both errors by the fp32 kernel's against fp64);
@@ -167,13 +167,13 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
       "fp16x2": fp32-accurate with half of split3's products: both operands as an fp16
                hi + lo pair after exact power-of-two scaling (per layer for the weights, per
                board for the inputs), three products in fp32 (csrc/conv_wino4.hip, 128
-               channels; 64-channel convs fall back to split3);
+               channels; 64-channel convs fall back to split3) -- the default for fp32;
       "fp16":  fp16 operands, fp32 accumulation (config #5's fp16 inference; the default
                when dtype is float16).
     Activations, the stem and the heads stay fp32 on the fused path.  conv_algo ("direct" /
     "wino") overrides default_conv_algo for the 16-bit trunk."""
     if precision is None:
-        precision = "fp16" if dtype == torch.float16 else "split3"
+        precision = "fp16" if dtype == torch.float16 else "fp16x2"
     assert precision in ("split3", "fp16x2", "fp32", "fp16"), precision
     import copy
 
@@ -284,10 +284,13 @@ class _HipConv3x3(nn.Module):
                       "conv3x3 weight prep")
             self.wq = nn.Parameter(wq, requires_grad=False)
 
-    def forward(self, x, res=None, relu=True, in_absmax=None, out_absmax=None):
+    def forward(self, x, res=None, relu=True, in_absmax=None, out_absmax=None, part=None,
+                splits=0):
         """in_absmax / out_absmax: float [B] per-board max |x| (consumed: reset to 0) and
         max |y| accumulator (zeros on entry) of the wino4 kernel; fp16x2 needs in_absmax
-        (computed here when absent)."""
+        (computed here when absent).  splits (2 or 4, fp16x2 only) with part (float
+        [splits * B * 64 * C]): the channel-split form for small batches
+        (az_conv3x3_wino4_splitk_gpu)."""
         import az_native as nat
 
         x = x.contiguous(memory_format=torch.channels_last)
@@ -298,6 +301,12 @@ class _HipConv3x3(nn.Module):
         if self.algo == "wino4":
             if self.precision == "fp16x2" and in_absmax is None:
                 in_absmax = board_absmax(x)
+            if splits and self.precision == "fp16x2":
+                nat.check(nat.lib.az_conv3x3_wino4_splitk_gpu(
+                    nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp, nat.ptr(y), x.shape[0],
+                    self.channels, int(relu), self.mode, nat.ptr(in_absmax), nat.ptr(out_absmax),
+                    nat.ptr(part), splits, nat.stream_ptr()), "az_conv3x3_wino4_splitk_gpu")
+                return y
             nat.check(nat.lib.az_conv3x3_wino4_gpu(
                 nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), rp, nat.ptr(y), x.shape[0],
                 self.channels, int(relu), self.mode, nat.ptr(in_absmax), nat.ptr(out_absmax),
@@ -418,6 +427,22 @@ class FusedInferenceNet(nn.Module, Inference):
     # than the layer-by-layer graph at the bench batch (scripts/trunk_bench.py,
     # profiles/r01_trunk_bench.jsonl), so off by default
     fuse_trunk = False
+    # fp16x2 trunk at small batches (a search's few leaves per step): the channel-split conv
+    # (az_conv3x3_wino4_splitk_gpu) puts `splits` workgroups on each four boards.  Per-launch
+    # times (scripts/splitk_sweep.py, profiles/r02_splitk_sweep.jsonl; one-pass / 4 / 8
+    # splits): 4 boards 32.0 / 15.4 / 13.3 us, 32: 32.6 / 19.4 / 19.1, 128: 32.8 / 26.1 /
+    # 28.4, 256: 33.1 / 31.5 / 41.6.  AZ_SPLITK=<splits> (0 = off) forces one form.
+    splitk_table = ((32, 8), (128, 4))  # (max boards, splits)
+
+    @classmethod
+    def splitk_for(cls, n_boards):
+        env = os.environ.get("AZ_SPLITK")
+        if env is not None:
+            return int(env)
+        for max_b, splits in cls.splitk_table:
+            if n_boards <= max_b:
+                return splits
+        return 0
 
     def _trunk_kernel_ready(self):
         """Whether the single-launch trunk (az_trunk_wino_gpu) applies: HIP stem and every
@@ -476,9 +501,18 @@ class FusedInferenceNet(nn.Module, Inference):
             else:
                 h = self.stem(x)
                 board_absmax(h, out=bufs[0])
+            sk = {}
+            splits = self.splitk_for(B)
+            if splits and all(c.algo == "wino4" for c in c1s + c2s):
+                part = getattr(self, "_splitk_part", None)
+                n = splits * B * 64 * c1s[0].channels
+                if part is None or part.numel() != n or part.device != x.device:
+                    part = self._splitk_part = torch.empty(n, dtype=torch.float32,
+                                                           device=x.device)
+                sk = {"part": part, "splits": splits}
             for c1, c2 in zip(c1s, c2s):
-                t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1])
-                h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0])
+                t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)
+                h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0], **sk)
             return h
         else:
             h = self.stem(x)

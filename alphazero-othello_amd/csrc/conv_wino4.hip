@@ -101,7 +101,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-template <int MODE_, int NRT_, int BOARDS_ = 4>
+template <int MODE_, int NRT_, int BOARDS_ = 4, int NC_ = 8>
 struct W4 {
   static constexpr int C = 128, MODE = MODE_;
   static constexpr int PLANES =
@@ -134,6 +134,13 @@ struct W4 {
   static constexpr int CHUNKS = C / 16;
   static constexpr int LCHUNKS = 4 * CHUNKS;        // (group, chunk) pairs
   static constexpr int QSTEPS = LCHUNKS * 4;        // (group, chunk, point) steps
+  // Channel split (small batches, az_conv3x3_wino4_splitk_gpu): a workgroup runs NC of the
+  // CHUNKS input-channel chunks of every group -- chunks cs .. cs + NC - 1, cs = NC *
+  // blockIdx.y -- and writes its partial output sums; a second kernel adds the splits in
+  // order with the epilogue.  Its own chunk sequence is the "virtual" index v = 0 .. VCH-1.
+  static constexpr int NC = NC_, VCH = 4 * NC, VQ = VCH * 4;
+  static constexpr bool SPLIT = NC < CHUNKS;
+  static_assert((NC == 1 || NC % 2 == 0) && CHUNKS % NC == 0, "chunk pairs per split");
   // weight fragment ring and prefetch distance (steps)
   static constexpr int PD = MODE == AZ_CONV_FP16 ? AZ_W4_PD16 : AZ_W4_PD3;
   static constexpr int RING = PD < 4 ? 4 : 8;  // divides the 8 steps of a chunk pair
@@ -358,12 +365,27 @@ struct St {
   int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], cols[G::TPT], soff[G::TPT], aoff[G::NRT];
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
   int wlane, tid, b0, nb;
+  int cs;             // first channel chunk of this workgroup's split (0 unless SPLIT)
   unsigned lds_res;   // LDS byte address of this wave's first residual piece
   const float* x;
   const float* res;
   const char* wq;
   char* lds;
 };
+
+// virtual chunk v of this workgroup -> linear chunk L = (group, channel chunk); clamped to the
+// last one (the pipeline's look-ahead past the end reads a duplicate, as before)
+template <class G>
+__device__ __forceinline__ int lmap(const St<G>& S, int v) {
+  v = v < G::VCH ? v : G::VCH - 1;
+  return (v / G::NC) * G::CHUNKS + S.cs + (v % G::NC);
+}
+// virtual step vq (= 4 v + point) -> linear weight step
+template <class G>
+__device__ __forceinline__ int qmap(const St<G>& S, int vq) {
+  vq = vq < G::VQ ? vq : G::VQ - 1;
+  return lmap<G>(S, vq >> 2) * 4 + (vq & 3);
+}
 
 // one 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane i's 16 bytes land at LDS
 // byte address lds_dst + 16 i.  Issued as asm so the compiler's vmcnt bookkeeping for the
@@ -399,14 +421,15 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // four steps, the next chunk's transform into the other LDS buffer, the windows of the
 // chunk after that requested
 template <class G, int PAR, int STAGE>
-__device__ __forceinline__ void run_chunk(St<G>& S, int L) {
-  const char* cur = S.lds + (L & 1) * G::BUF;
-  char* nxt = S.lds + ((L + 1) & 1) * G::BUF;
-  // chunk L+1's rows (its windows were requested during chunk L-1); the last chunk
+__device__ __forceinline__ void run_chunk(St<G>& S, int v) {
+  const int L = lmap<G>(S, v);
+  const char* cur = S.lds + (v & 1) * G::BUF;
+  char* nxt = S.lds + ((v + 1) & 1) * G::BUF;
+  // chunk v+1's rows (its windows were requested during chunk v-1); the last chunk
   // transforms a clamped duplicate into the idle buffer (uniform body)
-  const int Lr = L + 1 < G::LCHUNKS ? L + 1 : G::LCHUNKS - 1;
-  const int Ll = L + 1 + G::IPD < G::LCHUNKS ? L + 1 + G::IPD : G::LCHUNKS - 1;  // loaded
-  const int Ls = L + 2 < G::LCHUNKS ? L + 2 : G::LCHUNKS - 1;                    // stored
+  const int Lr = lmap<G>(S, v + 1);
+  const int Ll = lmap<G>(S, v + 1 + G::IPD);  // loaded
+  const int Ls = lmap<G>(S, v + 2);           // stored (slot (v + 2) & 1 = v & 1)
   constexpr int set_l = G::IPD == 1 ? 0 : (PAR + 1) & 1, set_s = G::IPD == 1 ? 0 : PAR;
 #pragma unroll
   for (int l = 0; l < 4; ++l) {
@@ -429,9 +452,8 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
 #pragma unroll
       for (int u = 0; u < G::TPT; ++u) combine_rows(S.rk[u], S.dr[u], Lr);
     }
-    const int q = L * 4 + l + G::PD;
     if (!(AZ_W4_EXP & 1))
-      load_b<G>(S.bf[(slot + G::PD) % G::RING], S.wq, S.wlane, q < G::QSTEPS - 1 ? q : G::QSTEPS - 1);
+      load_b<G>(S.bf[(slot + G::PD) % G::RING], S.wq, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
     // the chunk-after-next's input slice at the chunk's first step: four steps of latency
     // cover before it is stored to LDS at the chunk's end
     if (l == 0 && !(AZ_W4_EXP & 2)) load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
@@ -463,14 +485,14 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int L) {
 #endif
     __builtin_amdgcn_sched_barrier(0);
   }
-  // slot (L+2) & 1 = L & 1 held chunk L's input, whose rows were formed in chunk L-1
-  if (!(AZ_W4_EXP & 2)) store_in<G>(S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
+  // slot (v+2) & 1 = v & 1 held chunk v's input, whose rows were formed in chunk v-1
+  if (!(AZ_W4_EXP & 2)) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
   if (!(AZ_W4_EXP & 8)) lds_barrier();
   read_a<G>(S.af, nxt, 0, S.aoff);
   // the next chunk's window rows (chunk L+2, stored just before the barrier)
 #pragma unroll
   for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (Ls & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
 }
 
 template <class G>
@@ -487,10 +509,14 @@ __device__ __forceinline__ void zero_acc(St<G>& S) {
 // none for -1), then the fold
 template <class G, int K, int STAGE = -1>
 __device__ __forceinline__ void run_group(St<G>& S) {
+  if constexpr (G::NC == 1) {
+    run_chunk<G, K & 1, STAGE>(S, K);  // one chunk per group: the parity alternates by group
+  } else {
 #pragma unroll 1
-  for (int c = 0; c < G::CHUNKS; c += 2) {
-    run_chunk<G, 0, STAGE>(S, K * G::CHUNKS + c);
-    run_chunk<G, 1, STAGE>(S, K * G::CHUNKS + c + 1);
+    for (int c = 0; c < G::NC; c += 2) {
+      run_chunk<G, 0, STAGE>(S, K * G::NC + c);
+      run_chunk<G, 1, STAGE>(S, K * G::NC + c + 1);
+    }
   }
   fold<G, K>(S.acc, S.Y);
   zero_acc<G>(S);
@@ -558,6 +584,8 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   S.tid = tid;
   S.b0 = b0;
   S.nb = nb;
+  S.cs = G::SPLIT ? (int)blockIdx.y * G::NC : 0;
+  if constexpr (G::SPLIT) y += (size_t)blockIdx.y * n_boards * 64 * C;  // this split's partials
   S.lds_res = (unsigned)(uintptr_t)(S.lds + G::RES_OFF) + 16 * 64 * wave;
   S.wlane = (col0 + r) * 32 + h * 16;
 #pragma unroll
@@ -606,18 +634,18 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
       *reinterpret_cast<f32x4*>(in0 + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 ld0[G::LD_PER_THREAD], ld1[G::LD_PER_THREAD];
-    load_in<G>(ld0, x, S.goff, 0);
-    load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, x, S.goff, 1);
-    if (G::IPD == 2) load_in<G>(S.ld[0], x, S.goff, 2);  // stored at the end of chunk 0
+    load_in<G>(ld0, x, S.goff, lmap<G>(S, 0));
+    load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, x, S.goff, lmap<G>(S, 1));
+    if (G::IPD == 2) load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));  // stored at the end of chunk 0
 #pragma unroll
-    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, i);
+    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, qmap<G>(S, i));
     lds_barrier();  // the zero fill before any interior store
     store_in<G>(in0, ld0, S.ldst);
     store_in<G>(in0 + G::IN_SLOT, G::IPD == 1 ? S.ld[0] : ld1, S.ldst);
-    if (G::IPD == 1) load_in<G>(S.ld[0], x, S.goff, 2);  // stored at the end of chunk 0
+    if (G::IPD == 1) load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));  // stored at the end of chunk 0
     lds_barrier();
 #pragma unroll
-    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], S.cols[u], 0);
+    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], S.cols[u], lmap<G>(S, 0));
   }
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u) {
@@ -632,12 +660,12 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   read_a<G>(S.af, S.lds, 0, S.aoff);
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], S.cols[u], 1);
+    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], S.cols[u], lmap<G>(S, 1));
   // epilogue constants: bias, and (FP16X2) the scale M carries, 2^(su + sv_board); removing
   // it is an exact power-of-two product
   Epi<G> E;
   E.co = col0 + r;
-  E.bv = bias[E.co];
+  E.bv = G::SPLIT ? 0.0f : bias[E.co];  // split partials: bias etc. in the combining kernel
 #pragma unroll
   for (int i = 0; i < 2 * G::NRT; ++i) {
     E.unsc[i] = 1.0f;
@@ -661,7 +689,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   W4_STAMP(3);
   // output rows 2ty (Y[0]) are final after group 2: stored while group 3 computes, with
   // their residual staged through LDS during group 2 (and the odd rows' during group 3)
-  constexpr bool STAGED = RES && G::RES_FITS;
+  constexpr bool STAGED = RES && G::RES_FITS && !G::SPLIT;
   run_group<G, 2, STAGED ? 0 : -1>(S);
   W4_STAMP(4);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
@@ -684,7 +712,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   }
   // in_absmax is consumed: reset for its next use as some layer's out_absmax (every thread
   // read its entries in the prologue, before the first barrier)
-  if (G::SCALED && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
+  if (G::SCALED && !G::SPLIT && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
   W4_STAMP(6);
 }
 
@@ -718,7 +746,108 @@ int launch_wino4(const float* x, const void* wq, const float* bias, const float*
   return AZ_OK;
 }
 
+// split-K second pass: y = act(sum over splits s = 0, 1, .. in order of part[s] + bias (+ res));
+// grid (boards, 4 quarters of a board); out_absmax[b] gets the board's max |y| (zeros on
+// entry, as for the one-pass kernel), in_absmax[b] is consumed (reset to 0)
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void k_splitk_combine(
+    const float* __restrict__ part, int splits, const float* __restrict__ bias,
+    const float* __restrict__ res, float* __restrict__ y, int n_boards,
+    float* __restrict__ in_absmax, float* __restrict__ out_absmax) {
+  constexpr int C = 128, PER = 64 * C / 4;  // floats per (board, quarter)
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t base = (size_t)b * 64 * C + (size_t)blockIdx.y * PER;
+  const size_t stride = (size_t)n_boards * 64 * C;
+  float m = 0.0f;
+#pragma unroll
+  for (int k = 0; k < PER / 4 / 256; ++k) {
+    const int i = 4 * (tid + 256 * k);
+    const size_t o = base + i;
+    float4 v = *reinterpret_cast<const float4*>(part + o);
+    for (int s = 1; s < splits; ++s) {
+      const float4 p = *reinterpret_cast<const float4*>(part + s * stride + o);
+      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    }
+    const float4 bv = *reinterpret_cast<const float4*>(bias + (i & (C - 1)));
+    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+    if (RES) {
+      const float4 r = *reinterpret_cast<const float4*>(res + o);
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    if (RELU) {
+      v.x = fmaxf(v.x, 0.0f); v.y = fmaxf(v.y, 0.0f); v.z = fmaxf(v.z, 0.0f); v.w = fmaxf(v.w, 0.0f);
+    }
+    *reinterpret_cast<float4*>(y + o) = v;
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  if (out_absmax) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((tid & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(out_absmax) + b, __float_as_uint(m));
+  }
+  if (in_absmax && blockIdx.y == 0 && tid == 0) in_absmax[b] = 0.0f;
+}
+
+// small batches: the channel chunks split over `splits` workgroups per board group (NC =
+// CHUNKS / splits chunks each), partial sums to `part`, then k_splitk_combine
+template <int NC>
+int launch_wino4_splitk(const float* x, const void* wq, const float* bias, const float* res,
+                        float* y, int n_boards, int relu, float* in_absmax, float* out_absmax,
+                        float* part, hipStream_t s) {
+  using G = W4<AZ_CONV_FP16X2, 1, 4, NC>;
+  constexpr int splits = G::CHUNKS / NC;
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_conv3x3_wino4<G, false, false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  const dim3 grid((unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS), splits);
+  hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), grid, dim3(G::THREADS),
+                     (size_t)G::LDS_BYTES, s, x, static_cast<const char*>(wq), bias, nullptr,
+                     part, n_boards, in_absmax, nullptr);
+  AZ_HIP(hipGetLastError());
+  const dim3 cg((unsigned)n_boards, 4);
+  if (res && relu)
+    hipLaunchKernelGGL((k_splitk_combine<true, true>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+  else if (res)
+    hipLaunchKernelGGL((k_splitk_combine<true, false>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+  else if (relu)
+    hipLaunchKernelGGL((k_splitk_combine<false, true>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+  else
+    hipLaunchKernelGGL((k_splitk_combine<false, false>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
 }  // namespace
+
+extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const float* bias,
+                                           const float* res, float* y, int32_t n_boards,
+                                           int32_t channels, int32_t relu, int32_t mode,
+                                           float* in_absmax, float* out_absmax, float* part,
+                                           int32_t splits, void* stream) {
+  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: n_boards < 0");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(x && wq && bias && y && part && in_absmax && x != y && (!res || res != y) &&
+                 in_absmax != out_absmax,
+             AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: null buffer or in-place call");
+  AZ_REQUIRE(((uintptr_t)x | (uintptr_t)wq | (uintptr_t)bias | (uintptr_t)y | (uintptr_t)part |
+              (uintptr_t)res) % 16 == 0,
+             AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(channels == 128 && mode == AZ_CONV_FP16X2, AZ_ERR_ARG,
+             "az_conv3x3_wino4_splitk_gpu: 128 channels, FP16X2 only (got %d, mode %d)",
+             channels, mode);
+  hipStream_t s = azc::as_stream(stream);
+  if (splits == 2)
+    return launch_wino4_splitk<4>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
+  if (splits == 4)
+    return launch_wino4_splitk<2>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
+  if (splits == 8)
+    return launch_wino4_splitk<1>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
+  return azc::set_error(AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4 or 8, got %d",
+                        splits);
+}
 
 #if AZ_W4_STAMP
 extern "C" int az_w4_stamps(unsigned long long* host, int n) {

@@ -251,8 +251,8 @@ class BatchedSelfPlay:
 
     `net` is any module with the reference forward signature ([B,1,8,8] -> (logits [B,65],
     value [B,1])); it is evaluated through `Models.inference_copy` (BatchNorm folded,
-    channels-last, trunk `precision` "split3" (fp32-accurate, default) / "fp32" / "fp16" =
-    config #5).  `args` uses the reference's keys
+    channels-last, trunk `precision` "fp16x2" (fp32-accurate, default for fp32) / "split3" / "fp32" /
+    "fp16" = config #5).  `args` uses the reference's keys
     (train.py:399-423): c_puct, num_simulations, dirichlet_alpha, dirichlet_epsilon,
     mcts_temperature, num_exploratory_moves, lambda.
     """

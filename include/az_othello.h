@@ -347,6 +347,18 @@ int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias, cons
                          float* y, int32_t n_boards, int32_t channels, int32_t relu,
                          int32_t mode, float* in_absmax, float* out_absmax, void* stream);
 
+/* az_conv3x3_wino4_gpu (FP16X2, 128 channels) for small batches -- a search's few leaves per
+ * step, where one workgroup per four boards leaves the chip idle: the 128 input channels are
+ * split over `splits` (2, 4 or 8) workgroups per board group, each writing its partial sums to
+ * part (float [splits][n_boards][64][128]), and a second kernel adds the splits in order
+ * with bias / residual / ReLU and the max |y| of each board.  Same in_absmax / out_absmax
+ * contract; fp32 sums of the same products in a different order (not bit-identical to the
+ * one-pass kernel). */
+int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const float* bias,
+                                const float* res, float* y, int32_t n_boards, int32_t channels,
+                                int32_t relu, int32_t mode, float* in_absmax, float* out_absmax,
+                                float* part, int32_t splits, void* stream);
+
 /* out[b] = max |x[b][.]| over each board's 64 * channels fp32 values (NHWC): the
  * in_absmax of az_conv3x3_wino4_gpu for a tensor no kernel produced it for. */
 int az_board_absmax_gpu(const float* x, int32_t n_boards, int32_t channels, float* out,

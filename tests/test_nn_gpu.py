@@ -103,6 +103,31 @@ def test_inference_copy_matches_module(kind, conv, precision, algo):
     torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("B", [1, 4, 33, 128, 129])
+def test_inference_copy_fp16x2_small_batches(B):
+    """The default fp32 inference copy (fp16x2 trunk) at a search's batch sizes: up to 32
+    boards the trunk runs the 8-way channel-split conv, up to 128 the 4-way one, above it the
+    one-pass kernel; all match the module at the fp32 tolerance."""
+    from Models import FusedInferenceNet
+
+    torch.manual_seed(1)
+    net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    assert fused.precision == "fp16x2"
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    with torch.no_grad():
+        logits, v = net(x.view(-1, 1, 8, 8))
+        p, val = fused.evaluate_planes(x)
+    splits = FusedInferenceNet.splitk_for(B)
+    assert splits == (8 if B <= 32 else 4 if B <= 128 else 0)
+    part = getattr(fused, "_splitk_part", None)
+    assert (part is not None) == bool(splits)
+    if splits:
+        assert part.numel() == splits * B * 64 * 128
+    torch.testing.assert_close(p, torch.softmax(logits, -1), atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
+
+
 def _mx_conv(x, w, b, r, relu, mode):
     C = x.shape[1]
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
@@ -118,7 +143,8 @@ def _mx_conv(x, w, b, r, relu, mode):
     return y
 
 
-def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu", out_absmax=None):
+def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu", out_absmax=None, splits=0,
+               in_absmax=None):
     C = x.shape[1]
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
     wq = torch.empty(nat.lib.az_conv3x3_wino_prep_bytes(C, mode) // 2, dtype=torch.int16,
@@ -131,7 +157,13 @@ def _wino_conv(x, w, b, r, relu, mode, fn="az_conv3x3_wino_gpu", out_absmax=None
     if fn == "az_conv3x3_wino4_gpu":
         from Models import board_absmax
 
-        args += [nat.ptr(board_absmax(x)), nat.ptr(out_absmax)]
+        if in_absmax is None:
+            in_absmax = board_absmax(x)
+        args += [nat.ptr(in_absmax), nat.ptr(out_absmax)]
+        if splits:
+            fn = "az_conv3x3_wino4_splitk_gpu"
+            part = torch.full((splits * x.numel(),), float("nan"), device="cuda")
+            args += [nat.ptr(part), splits]
     nat.check(getattr(nat.lib, fn)(*args, nat.stream_ptr()), fn)
     torch.cuda.synchronize()
     return y
@@ -223,13 +255,16 @@ def test_conv3x3_winograd4_is_fp32_accurate(B, res, relu):
     torch.testing.assert_close(y, ref.float().cuda(), **TOL)
 
 
+@pytest.mark.parametrize("splits", [0, 2, 4, 8])
 @pytest.mark.parametrize("B", [1, 3, 5, 130, 1024])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
-def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu):
+def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu, splits):
     """FP16X2 (fp16 hi + lo operand pairs after exact power-of-two scaling, three products)
     against fp64: the same fp32-accuracy bar as split3 (max |err| <= 2x the fp32 MFMA
     kernel's + 1e-6, mean <= 2x), boards of very different magnitude in one batch included
-    (the input scale is per board), and the per-board max |y| output exact."""
+    (the input scale is per board), and the per-board max |y| output exact.  splits = 2 / 4 / 8:
+    the channel-split small-batch form (az_conv3x3_wino4_splitk_gpu), which also consumes
+    in_absmax (reset to 0)."""
     C = 128
     x, w, b, r, ref64 = _case(C, B, C * 23 + B)
     if B > 1:  # per-board ranges from 1e-3 to 1e3
@@ -238,8 +273,12 @@ def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu):
         ref64 = F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), padding=1)
     rr = r if res else None
     amax = torch.zeros(B, dtype=torch.float32, device="cuda")
+    from Models import board_absmax
+
+    in_amax = board_absmax(x)
     y = _wino_conv(x, w, b, rr, relu, nat.AZ_CONV_FP16X2, fn="az_conv3x3_wino4_gpu",
-                   out_absmax=amax)
+                   out_absmax=amax, splits=splits, in_absmax=in_amax)
+    assert (in_amax == 0).all()
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
     y32 = torch.empty_like(x, memory_format=torch.channels_last)
     nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
