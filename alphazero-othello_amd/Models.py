@@ -430,9 +430,9 @@ class FusedInferenceNet(nn.Module, Inference):
     # fp16x2 trunk at small batches (a search's few leaves per step): the channel-split conv
     # (az_conv3x3_wino4_splitk_gpu) puts `splits` workgroups on each four boards.  Per-launch
     # times (scripts/splitk_sweep.py, profiles/r02_splitk_sweep.jsonl; one-pass / 4 / 8
-    # splits): 4 boards 32.0 / 15.4 / 13.3 us, 32: 32.6 / 19.4 / 19.1, 128: 32.8 / 26.1 /
-    # 28.4, 256: 33.1 / 31.5 / 41.6.  AZ_SPLITK=<splits> (0 = off) forces one form.
-    splitk_table = ((32, 8), (128, 4))  # (max boards, splits)
+    # splits): 4 boards 32.0 / 14.3 / 11.4 us, 32: 32.4 / 17.4 / 15.6, 128: 32.7 / 24.2 /
+    # 25.1, 256: 33.9 / 28.0 / 37.4.  AZ_SPLITK=<splits> (0 = off) forces one form.
+    splitk_table = ((32, 8), (256, 4))  # (max boards, splits)
 
     @classmethod
     def splitk_for(cls, n_boards):

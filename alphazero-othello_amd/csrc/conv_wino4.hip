@@ -746,46 +746,50 @@ int launch_wino4(const float* x, const void* wq, const float* bias, const float*
   return AZ_OK;
 }
 
-// split-K second pass: y = act(sum over splits s = 0, 1, .. in order of part[s] + bias (+ res));
-// grid (boards, 4 quarters of a board); out_absmax[b] gets the board's max |y| (zeros on
-// entry, as for the one-pass kernel), in_absmax[b] is consumed (reset to 0)
-template <bool RES, bool RELU>
+// split-K second pass: y = act(sum over splits s = 0 .. S-1 in order of part[s] + bias (+ res));
+// one float4 per thread, every split's load issued before the sums (the pass is load-latency
+// bound at a search's few boards), 8 workgroups per board; out_absmax[b] gets the board's
+// max |y| (zeros on entry, as for the one-pass kernel), in_absmax[b] is consumed (reset to 0)
+template <int S, bool RES, bool RELU>
 __global__ __launch_bounds__(256) void k_splitk_combine(
-    const float* __restrict__ part, int splits, const float* __restrict__ bias,
+    const float* __restrict__ part, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
     float* __restrict__ in_absmax, float* __restrict__ out_absmax) {
-  constexpr int C = 128, PER = 64 * C / 4;  // floats per (board, quarter)
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const size_t base = (size_t)b * 64 * C + (size_t)blockIdx.y * PER;
+  constexpr int C = 128, WG_PER_BOARD = 64 * C / 4 / 256;
+  const int tid = threadIdx.x, b = blockIdx.x / WG_PER_BOARD;
+  const size_t o = 4 * ((size_t)blockIdx.x * 256 + tid);
   const size_t stride = (size_t)n_boards * 64 * C;
-  float m = 0.0f;
+  float4 p[S];
 #pragma unroll
-  for (int k = 0; k < PER / 4 / 256; ++k) {
-    const int i = 4 * (tid + 256 * k);
-    const size_t o = base + i;
-    float4 v = *reinterpret_cast<const float4*>(part + o);
-    for (int s = 1; s < splits; ++s) {
-      const float4 p = *reinterpret_cast<const float4*>(part + s * stride + o);
-      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-    }
-    const float4 bv = *reinterpret_cast<const float4*>(bias + (i & (C - 1)));
-    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-    if (RES) {
-      const float4 r = *reinterpret_cast<const float4*>(res + o);
-      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-    }
-    if (RELU) {
-      v.x = fmaxf(v.x, 0.0f); v.y = fmaxf(v.y, 0.0f); v.z = fmaxf(v.z, 0.0f); v.w = fmaxf(v.w, 0.0f);
-    }
-    *reinterpret_cast<float4*>(y + o) = v;
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  for (int s = 0; s < S; ++s) p[s] = *reinterpret_cast<const float4*>(part + s * stride + o);
+  const float4 bv = *reinterpret_cast<const float4*>(bias + (o & (C - 1)));
+  float4 r = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (RES) r = *reinterpret_cast<const float4*>(res + o);
+  float4 v = p[0];
+#pragma unroll
+  for (int s = 1; s < S; ++s) {
+    v.x += p[s].x; v.y += p[s].y; v.z += p[s].z; v.w += p[s].w;
   }
+  v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+  if (RES) {
+    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  }
+  if (RELU) {
+    v.x = fmaxf(v.x, 0.0f); v.y = fmaxf(v.y, 0.0f); v.z = fmaxf(v.z, 0.0f); v.w = fmaxf(v.w, 0.0f);
+  }
+  *reinterpret_cast<float4*>(y + o) = v;
   if (out_absmax) {
+    float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-    if ((tid & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(out_absmax) + b, __float_as_uint(m));
+    __shared__ float s_m[4];
+    if ((tid & 63) == 0) s_m[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0)
+      atomicMax(reinterpret_cast<unsigned*>(out_absmax) + b,
+                __float_as_uint(fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]))));
   }
-  if (in_absmax && blockIdx.y == 0 && tid == 0) in_absmax[b] = 0.0f;
+  if (in_absmax && blockIdx.x % WG_PER_BOARD == 0 && tid == 0) in_absmax[b] = 0.0f;
 }
 
 // small batches: the channel chunks split over `splits` workgroups per board group (NC =
@@ -807,15 +811,15 @@ int launch_wino4_splitk(const float* x, const void* wq, const float* bias, const
                      (size_t)G::LDS_BYTES, s, x, static_cast<const char*>(wq), bias, nullptr,
                      part, n_boards, in_absmax, nullptr);
   AZ_HIP(hipGetLastError());
-  const dim3 cg((unsigned)n_boards, 4);
+  const dim3 cg((unsigned)n_boards * (64 * 128 / 4 / 256));
   if (res && relu)
-    hipLaunchKernelGGL((k_splitk_combine<true, true>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_splitk_combine<splits, true, true>), cg, dim3(256), 0, s, part, bias, res, y, n_boards, in_absmax, out_absmax);
   else if (res)
-    hipLaunchKernelGGL((k_splitk_combine<true, false>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_splitk_combine<splits, true, false>), cg, dim3(256), 0, s, part, bias, res, y, n_boards, in_absmax, out_absmax);
   else if (relu)
-    hipLaunchKernelGGL((k_splitk_combine<false, true>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_splitk_combine<splits, false, true>), cg, dim3(256), 0, s, part, bias, res, y, n_boards, in_absmax, out_absmax);
   else
-    hipLaunchKernelGGL((k_splitk_combine<false, false>), cg, dim3(256), 0, s, part, splits, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_splitk_combine<splits, false, false>), cg, dim3(256), 0, s, part, bias, res, y, n_boards, in_absmax, out_absmax);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

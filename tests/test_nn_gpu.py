@@ -103,10 +103,10 @@ def test_inference_copy_matches_module(kind, conv, precision, algo):
     torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("B", [1, 4, 33, 128, 129])
+@pytest.mark.parametrize("B", [1, 4, 33, 256, 257])
 def test_inference_copy_fp16x2_small_batches(B):
     """The default fp32 inference copy (fp16x2 trunk) at a search's batch sizes: up to 32
-    boards the trunk runs the 8-way channel-split conv, up to 128 the 4-way one, above it the
+    boards the trunk runs the 8-way channel-split conv, up to 256 the 4-way one, above it the
     one-pass kernel; all match the module at the fp32 tolerance."""
     from Models import FusedInferenceNet
 
@@ -119,7 +119,7 @@ def test_inference_copy_fp16x2_small_batches(B):
         logits, v = net(x.view(-1, 1, 8, 8))
         p, val = fused.evaluate_planes(x)
     splits = FusedInferenceNet.splitk_for(B)
-    assert splits == (8 if B <= 32 else 4 if B <= 128 else 0)
+    assert splits == (8 if B <= 32 else 4 if B <= 256 else 0)
     part = getattr(fused, "_splitk_part", None)
     assert (part is not None) == bool(splits)
     if splits:
