@@ -1984,8 +1984,15 @@ int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
   // leaves, another legal interleaving of the reference's workers)
   const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4 * e->p.K)
                                           : 4 * (e->p.sims + 1) + 64;
+  // the kernels' per-leaf arrays sized to the next power of two >= K (registers)
   if (e->p.K == 1)
     hipLaunchKernelGGL(k_select<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
+                       leaf_o, max_descents);
+  else if (e->p.K <= 2)
+    hipLaunchKernelGGL(k_select<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
+                       leaf_o, max_descents);
+  else if (e->p.K <= 4)
+    hipLaunchKernelGGL(k_select<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
                        leaf_o, max_descents);
   else
     hipLaunchKernelGGL(k_select<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
@@ -2005,6 +2012,12 @@ int az_expand_backup(az_engine* e, const float* priors, const float* values, voi
   }
   if (e->p.K == 1)
     hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
+                       values);
+  else if (e->p.K <= 2)
+    hipLaunchKernelGGL(k_expand<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
+                       values);
+  else if (e->p.K <= 4)
+    hipLaunchKernelGGL(k_expand<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
                        values);
   else
     hipLaunchKernelGGL(k_expand<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
