@@ -429,10 +429,11 @@ class FusedInferenceNet(nn.Module, Inference):
     fuse_trunk = False
     # fp16x2 trunk at small batches (a search's few leaves per step): the channel-split conv
     # (az_conv3x3_wino4_splitk_gpu) puts `splits` workgroups on each four boards.  Per-launch
-    # times (scripts/splitk_sweep.py, profiles/r02_splitk_sweep.jsonl; one-pass / 4 / 8
-    # splits): 4 boards 32.0 / 14.3 / 11.4 us, 32: 32.4 / 17.4 / 15.6, 128: 32.7 / 24.2 /
-    # 25.1, 256: 33.9 / 28.0 / 37.4.  AZ_SPLITK=<splits> (0 = off) forces one form.
-    splitk_table = ((32, 8), (256, 4))  # (max boards, splits)
+    # times in 20-layer HIP graphs (scripts/splitk_sweep.py, profiles/r02_splitk_sweep.jsonl;
+    # one pass / 4 / 8 / 16 splits): 4 boards 32.0 / 13.6 / 10.8 / 9.4 us, 16: 32.6 / 15.4 /
+    # 13.6 / 13.8, 64: 33.0 / 19.5 / 20.4 / 23.6, 256: 34.4 / 27.5 / 37.8 / 62.1.
+    # AZ_SPLITK=<splits> (0 = off) forces one form.
+    splitk_table = ((8, 16), (32, 8), (256, 4))  # (max boards, splits)
 
     @classmethod
     def splitk_for(cls, n_boards):

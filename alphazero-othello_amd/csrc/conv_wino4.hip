@@ -101,7 +101,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-template <int MODE_, int NRT_, int BOARDS_ = 4, int NC_ = 8>
+template <int MODE_, int NRT_, int BOARDS_ = 4, int NC_ = 8, int NG_ = 4>
 struct W4 {
   static constexpr int C = 128, MODE = MODE_;
   static constexpr int PLANES =
@@ -138,9 +138,12 @@ struct W4 {
   // CHUNKS input-channel chunks of every group -- chunks cs .. cs + NC - 1, cs = NC *
   // blockIdx.y -- and writes its partial output sums; a second kernel adds the splits in
   // order with the epilogue.  Its own chunk sequence is the "virtual" index v = 0 .. VCH-1.
-  static constexpr int NC = NC_, VCH = 4 * NC, VQ = VCH * 4;
-  static constexpr bool SPLIT = NC < CHUNKS;
+  // NG = 1: the four transform-grid rows split over workgroups too (row g0 = blockIdx.y /
+  // (CHUNKS / NC)); the output transform is linear, so those partials add up as well.
+  static constexpr int NC = NC_, NG = NG_, VCH = NG * NC, VQ = VCH * 4;
+  static constexpr bool SPLIT = NC < CHUNKS || NG < 4;
   static_assert((NC == 1 || NC % 2 == 0) && CHUNKS % NC == 0, "chunk pairs per split");
+  static_assert(NG == 4 || NG == 1, "all four transform rows, or one");
   // weight fragment ring and prefetch distance (steps)
   static constexpr int PD = MODE == AZ_CONV_FP16 ? AZ_W4_PD16 : AZ_W4_PD3;
   static constexpr int RING = PD < 4 ? 4 : 8;  // divides the 8 steps of a chunk pair
@@ -324,14 +327,22 @@ __device__ __forceinline__ void fold(f32x16 (&acc)[4][G::NRT], f32x16 (&Y)[2][2]
     for (int e = 0; e < 16; ++e) {
       const float m0 = acc[0][t][e], m1 = acc[1][t][e], m2 = acc[2][t][e], m3 = acc[3][t][e];
       const float t0 = (m0 + m1) + m2, t1 = (m1 - m2) - m3;
-      if constexpr (K == 0) {
+      if constexpr (K == 0 && G::NG == 4) {
         Y[0][0][t][e] = t0;
         Y[0][1][t][e] = t1;
+      } else if constexpr (K == 0) {  // NG = 1: Y starts at zero (rows of other workgroups)
+        Y[0][0][t][e] += t0;
+        Y[0][1][t][e] += t1;
       } else if constexpr (K == 1) {
         Y[0][0][t][e] += t0;
         Y[0][1][t][e] += t1;
-        Y[1][0][t][e] = t0;
-        Y[1][1][t][e] = t1;
+        if constexpr (G::NG == 4) {
+          Y[1][0][t][e] = t0;
+          Y[1][1][t][e] = t1;
+        } else {
+          Y[1][0][t][e] += t0;
+          Y[1][1][t][e] += t1;
+        }
       } else if constexpr (K == 2) {
         Y[0][0][t][e] += t0;
         Y[0][1][t][e] += t1;
@@ -366,6 +377,7 @@ struct St {
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
   int wlane, tid, b0, nb;
   int cs;             // first channel chunk of this workgroup's split (0 unless SPLIT)
+  int g0;             // its transform-grid row (NG = 1; 0 otherwise)
   unsigned lds_res;   // LDS byte address of this wave's first residual piece
   const float* x;
   const float* res;
@@ -378,7 +390,7 @@ struct St {
 template <class G>
 __device__ __forceinline__ int lmap(const St<G>& S, int v) {
   v = v < G::VCH ? v : G::VCH - 1;
-  return (v / G::NC) * G::CHUNKS + S.cs + (v % G::NC);
+  return (S.g0 + v / G::NC) * G::CHUNKS + S.cs + (v % G::NC);
 }
 // virtual step vq (= 4 v + point) -> linear weight step
 template <class G>
@@ -509,13 +521,14 @@ __device__ __forceinline__ void zero_acc(St<G>& S) {
 // none for -1), then the fold
 template <class G, int K, int STAGE = -1>
 __device__ __forceinline__ void run_group(St<G>& S) {
+  constexpr int KV = G::NG == 4 ? K : 0;  // the group's place in this workgroup's sequence
   if constexpr (G::NC == 1) {
-    run_chunk<G, K & 1, STAGE>(S, K);  // one chunk per group: the parity alternates by group
+    run_chunk<G, KV & 1, STAGE>(S, KV);  // one chunk per group: the parity alternates by group
   } else {
 #pragma unroll 1
     for (int c = 0; c < G::NC; c += 2) {
-      run_chunk<G, 0, STAGE>(S, K * G::NC + c);
-      run_chunk<G, 1, STAGE>(S, K * G::NC + c + 1);
+      run_chunk<G, 0, STAGE>(S, KV * G::NC + c);
+      run_chunk<G, 1, STAGE>(S, KV * G::NC + c + 1);
     }
   }
   fold<G, K>(S.acc, S.Y);
@@ -584,7 +597,8 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   S.tid = tid;
   S.b0 = b0;
   S.nb = nb;
-  S.cs = G::SPLIT ? (int)blockIdx.y * G::NC : 0;
+  S.cs = G::SPLIT ? (int)(blockIdx.y % (G::CHUNKS / G::NC)) * G::NC : 0;
+  S.g0 = G::NG == 1 ? (int)(blockIdx.y / (G::CHUNKS / G::NC)) : 0;
   if constexpr (G::SPLIT) y += (size_t)blockIdx.y * n_boards * 64 * C;  // this split's partials
   S.lds_res = (unsigned)(uintptr_t)(S.lds + G::RES_OFF) + 16 * 64 * wave;
   S.wlane = (col0 + r) * 32 + h * 16;
@@ -683,6 +697,25 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   W4_STAMP(1);
   if (AZ_W4_PRIO == 1 && G::WAVES == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
     __builtin_amdgcn_s_setprio(1);
+  if constexpr (G::NG == 1) {  // one transform row: its partial outputs, both halves
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < G::NRT; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) S.Y[i][j][t][e] = 0.0f;
+    switch (S.g0) {
+      case 0: run_group<G, 0>(S); break;
+      case 1: run_group<G, 1>(S); break;
+      case 2: run_group<G, 2>(S); break;
+      default: run_group<G, 3>(S); break;
+    }
+    epilogue<G, 0, false, false>(S, E, res, y, rt0, h);
+    epilogue<G, 1, false, false>(S, E, res, y, rt0, h);
+    return;
+  } else {
   run_group<G, 0>(S);
   W4_STAMP(2);
   run_group<G, 1>(S);
@@ -714,6 +747,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   // read its entries in the prologue, before the first barrier)
   if (G::SCALED && !G::SPLIT && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
   W4_STAMP(6);
+  }
 }
 
 template <class G>
@@ -794,12 +828,12 @@ __global__ __launch_bounds__(256) void k_splitk_combine(
 
 // small batches: the channel chunks split over `splits` workgroups per board group (NC =
 // CHUNKS / splits chunks each), partial sums to `part`, then k_splitk_combine
-template <int NC>
+template <int NC, int NG = 4>
 int launch_wino4_splitk(const float* x, const void* wq, const float* bias, const float* res,
                         float* y, int n_boards, int relu, float* in_absmax, float* out_absmax,
                         float* part, hipStream_t s) {
-  using G = W4<AZ_CONV_FP16X2, 1, 4, NC>;
-  constexpr int splits = G::CHUNKS / NC;
+  using G = W4<AZ_CONV_FP16X2, 1, 4, NC, NG>;
+  constexpr int splits = G::CHUNKS / NC * (4 / NG);
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_conv3x3_wino4<G, false, false>,
@@ -849,7 +883,12 @@ extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const
     return launch_wino4_splitk<2>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
   if (splits == 8)
     return launch_wino4_splitk<1>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
-  return azc::set_error(AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4 or 8, got %d",
+  if (splits == 16)  // 4 transform rows x 4 channel splits
+    return launch_wino4_splitk<2, 1>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
+  if (splits == 32)  // 4 transform rows x 8 channel splits
+    return launch_wino4_splitk<1, 1>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, part, s);
+  return azc::set_error(AZ_ERR_ARG,
+                        "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4, 8, 16 or 32, got %d",
                         splits);
 }
 

@@ -349,11 +349,12 @@ int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias, cons
 
 /* az_conv3x3_wino4_gpu (FP16X2, 128 channels) for small batches -- a search's few leaves per
  * step, where one workgroup per four boards leaves the chip idle: the 128 input channels are
- * split over `splits` (2, 4 or 8) workgroups per board group, each writing its partial sums to
- * part (float [splits][n_boards][64][128]), and a second kernel adds the splits in order
- * with bias / residual / ReLU and the max |y| of each board.  Same in_absmax / out_absmax
- * contract; fp32 sums of the same products in a different order (not bit-identical to the
- * one-pass kernel). */
+ * split over 2, 4 or 8 workgroups per board group (splits = 16 or 32 also split the four
+ * Winograd transform rows, 4 x 4 or 4 x 8), each writing its partial sums to part (float
+ * [splits][n_boards][64][128]), and a second kernel adds the splits in order with bias /
+ * residual / ReLU and the max |y| of each board.  Same in_absmax / out_absmax contract; fp32
+ * sums of the same products in a different order (not bit-identical to the one-pass
+ * kernel). */
 int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const float* bias,
                                 const float* res, float* y, int32_t n_boards, int32_t channels,
                                 int32_t relu, int32_t mode, float* in_absmax, float* out_absmax,

@@ -103,11 +103,12 @@ def test_inference_copy_matches_module(kind, conv, precision, algo):
     torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("B", [1, 4, 33, 256, 257])
+@pytest.mark.parametrize("B", [1, 4, 9, 33, 257])
 def test_inference_copy_fp16x2_small_batches(B):
-    """The default fp32 inference copy (fp16x2 trunk) at a search's batch sizes: up to 32
-    boards the trunk runs the 8-way channel-split conv, up to 256 the 4-way one, above it the
-    one-pass kernel; all match the module at the fp32 tolerance."""
+    """The default fp32 inference copy (fp16x2 trunk) at a search's batch sizes: up to 8 boards
+    the trunk runs the 16-way split conv (channels x transform rows), up to 32 the 8-way
+    channel split, up to 256 the 4-way one, above it the one-pass kernel; all match the
+    module at the fp32 tolerance."""
     from Models import FusedInferenceNet
 
     torch.manual_seed(1)
@@ -119,7 +120,7 @@ def test_inference_copy_fp16x2_small_batches(B):
         logits, v = net(x.view(-1, 1, 8, 8))
         p, val = fused.evaluate_planes(x)
     splits = FusedInferenceNet.splitk_for(B)
-    assert splits == (8 if B <= 32 else 4 if B <= 256 else 0)
+    assert splits == (16 if B <= 8 else 8 if B <= 32 else 4 if B <= 256 else 0)
     part = getattr(fused, "_splitk_part", None)
     assert (part is not None) == bool(splits)
     if splits:
@@ -255,16 +256,16 @@ def test_conv3x3_winograd4_is_fp32_accurate(B, res, relu):
     torch.testing.assert_close(y, ref.float().cuda(), **TOL)
 
 
-@pytest.mark.parametrize("splits", [0, 2, 4, 8])
+@pytest.mark.parametrize("splits", [0, 2, 4, 8, 16, 32])
 @pytest.mark.parametrize("B", [1, 3, 5, 130, 1024])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
 def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu, splits):
     """FP16X2 (fp16 hi + lo operand pairs after exact power-of-two scaling, three products)
     against fp64: the same fp32-accuracy bar as split3 (max |err| <= 2x the fp32 MFMA
     kernel's + 1e-6, mean <= 2x), boards of very different magnitude in one batch included
-    (the input scale is per board), and the per-board max |y| output exact.  splits = 2 / 4 / 8:
-    the channel-split small-batch form (az_conv3x3_wino4_splitk_gpu), which also consumes
-    in_absmax (reset to 0)."""
+    (the input scale is per board), and the per-board max |y| output exact.  splits = 2 / 4 /
+    8 (channel chunks) or 16 / 32 (also the transform rows): the channel-split small-batch form
+    (az_conv3x3_wino4_splitk_gpu), which also consumes in_absmax (reset to 0)."""
     C = 128
     x, w, b, r, ref64 = _case(C, B, C * 23 + B)
     if B > 1:  # per-board ranges from 1e-3 to 1e3
