@@ -263,3 +263,15 @@ def test_bench_kernel_inputs_are_legal_playouts():
     assert ((lg[placed] >> act[placed].astype(np.uint64)) & np.uint64(1)).all()
     _, _, _, _, bad = ob.step_batch(own, opp, act)
     assert bad == -1
+
+
+def test_splitk_table_picks_the_measured_fastest_form(monkeypatch):
+    """FusedInferenceNet.splitk_for: the small-batch trunk conv form per batch size
+    (profiles/r02_splitk_sweep.jsonl), AZ_SPLITK overriding it."""
+    from Models import FusedInferenceNet as F
+
+    monkeypatch.delenv("AZ_SPLITK", raising=False)
+    want = {1: 16, 4: 16, 8: 16, 9: 8, 32: 8, 33: 4, 256: 4, 257: 0, 1024: 0}
+    assert {b: F.splitk_for(b) for b in want} == want
+    monkeypatch.setenv("AZ_SPLITK", "0")
+    assert F.splitk_for(4) == 0
