@@ -492,11 +492,15 @@ class FusedInferenceNet(nn.Module, Inference):
             # per-board input ranges ping-pong between two buffers: each conv consumes (and
             # resets) one and accumulates its output's into the other; the stem writes the
             # first (or, for a non-HIP stem, a separate max pass does)
+            # scratch kept per (device, batch size), never freed: a HIP graph captured at
+            # one batch size keeps pointing at its buffers while other sizes run eagerly
             B = x.shape[0]
-            bufs = getattr(self, "_absmax", None)
-            if bufs is None or bufs[0].shape[0] != B or bufs[0].device != x.device:
-                bufs = self._absmax = [torch.zeros(B, dtype=torch.float32, device=x.device)
-                                       for _ in range(2)]
+            scratch = self.__dict__.setdefault("_trunk_scratch", {})
+            key = (x.device, B)
+            if key not in scratch:
+                scratch[key] = {"absmax": [torch.zeros(B, dtype=torch.float32, device=x.device)
+                                           for _ in range(2)]}
+            bufs = scratch[key]["absmax"]
             if isinstance(self.stem, _HipStem):
                 h = self.stem(x, absmax=bufs[0])
             else:
@@ -505,11 +509,11 @@ class FusedInferenceNet(nn.Module, Inference):
             sk = {}
             splits = self.splitk_for(B)
             if splits and all(c.algo == "wino4" for c in c1s + c2s):
-                part = getattr(self, "_splitk_part", None)
                 n = splits * B * 64 * c1s[0].channels
-                if part is None or part.numel() != n or part.device != x.device:
-                    part = self._splitk_part = torch.empty(n, dtype=torch.float32,
-                                                           device=x.device)
+                part = scratch[key].get("part")
+                if part is None or part.numel() != n:
+                    part = scratch[key]["part"] = torch.empty(n, dtype=torch.float32,
+                                                              device=x.device)
                 sk = {"part": part, "splits": splits}
             for c1, c2 in zip(c1s, c2s):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)

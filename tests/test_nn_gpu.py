@@ -121,10 +121,14 @@ def test_inference_copy_fp16x2_small_batches(B):
         p, val = fused.evaluate_planes(x)
     splits = FusedInferenceNet.splitk_for(B)
     assert splits == (16 if B <= 8 else 8 if B <= 32 else 4 if B <= 256 else 0)
-    part = getattr(fused, "_splitk_part", None)
+    part = fused._trunk_scratch[(x.device, B)].get("part")
     assert (part is not None) == bool(splits)
     if splits:
         assert part.numel() == splits * B * 64 * 128
+    # another batch size gets its own scratch: a graph captured at B keeps valid pointers
+    with torch.no_grad():
+        fused.evaluate_planes(torch.zeros(B + 3, 64, device="cuda"))
+    assert fused._trunk_scratch[(x.device, B)].get("part") is part
     torch.testing.assert_close(p, torch.softmax(logits, -1), atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(val, v.reshape(-1), atol=1e-5, rtol=1e-4)
 
