@@ -301,6 +301,22 @@ def test_conv3x3_winograd4_fp16x2_is_fp32_accurate(B, res, relu, splits):
     assert torch.equal(amax.cpu(), y.abs().amax(dim=(1, 2, 3)).cpu())
 
 
+@pytest.mark.parametrize("splits", [4, 16])
+def test_conv3x3_winograd4_splitk_is_deterministic(splits):
+    """The split form adds its partials in a fixed order (no atomics on the data): two runs
+    on the same inputs are bit-identical, per-board max |y| included."""
+    from Models import board_absmax
+
+    x, w, b, r, _ = _case(128, 6, 128 * 31 + splits)
+    outs = []
+    for _ in range(2):
+        amax = torch.zeros(6, dtype=torch.float32, device="cuda")
+        y = _wino_conv(x, w, b, r, True, nat.AZ_CONV_FP16X2, fn="az_conv3x3_wino4_gpu",
+                       out_absmax=amax, splits=splits, in_absmax=board_absmax(x))
+        outs.append((y, amax))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_conv3x3_winograd4_fp16_mode():
     x, w, b, r, ref64 = _case(128, 37, 128 + 11)
     y = _wino_conv(x, w, b, r, True, nat.AZ_CONV_FP16, fn="az_conv3x3_wino4_gpu")
