@@ -222,11 +222,19 @@ class _EngineSearch:
         self._evaluate()
         e.expand()
 
+    # False: the same n iterations run eagerly (tests/test_callers_gpu.py compares the two)
+    use_graph = True
+
     def _run_on_device(self, n):
         """n select -> net -> expand iterations with no host synchronisation, replayed from
         one captured HIP graph of a single iteration (captured on first use)."""
         import torch
 
+        if not self.use_graph:
+            with torch.no_grad():
+                for _ in range(n):
+                    self._device_iteration()
+            return
         if getattr(self, "_graph", None) is None:
             s = torch.cuda.Stream(device=self.engine.device)
             s.wait_stream(torch.cuda.current_stream())

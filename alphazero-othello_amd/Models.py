@@ -463,6 +463,34 @@ class FusedInferenceNet(nn.Module, Inference):
                 "mode": convs[0].mode, "C": convs[0].channels, "blocks": len(self.c1)}
         return True
 
+    # eager-only batch sizes whose trunk scratch is kept (most recently used first out)
+    scratch_cap = 4
+
+    def _scratch(self, device, B):
+        """Trunk scratch (per-board ranges, split-K partials) of one (device, batch size).
+        Sizes seen while a HIP graph is being captured are pinned for the net's lifetime
+        (the graph keeps pointing at their buffers); at most `scratch_cap` other sizes are
+        kept, least recently used dropped first (a caller evaluating many ragged batch sizes
+        does not accumulate buffers).  release_scratch() drops the unpinned ones."""
+        sc = self.__dict__.setdefault("_trunk_scratch", {})
+        key = (device, B)
+        ent = sc.pop(key, None)  # re-inserted below: dict order = recency
+        if ent is None:
+            ent = {"absmax": [torch.zeros(B, dtype=torch.float32, device=device)
+                              for _ in range(2)], "pinned": False}
+        if torch.cuda.is_current_stream_capturing():
+            ent["pinned"] = True
+        sc[key] = ent
+        loose = [k for k, v in sc.items() if not v["pinned"]]
+        for k in loose[:max(0, len(loose) - self.scratch_cap)]:
+            del sc[k]  # stream-ordered free: queued work on this stream still sees it
+        return ent
+
+    def release_scratch(self):
+        sc = self.__dict__.get("_trunk_scratch", {})
+        for k in [k for k, v in sc.items() if not v["pinned"]]:
+            del sc[k]
+
     def _trunk(self, x):
         if x.dim() == 3:
             x = x.unsqueeze(1)
@@ -492,15 +520,9 @@ class FusedInferenceNet(nn.Module, Inference):
             # per-board input ranges ping-pong between two buffers: each conv consumes (and
             # resets) one and accumulates its output's into the other; the stem writes the
             # first (or, for a non-HIP stem, a separate max pass does)
-            # scratch kept per (device, batch size), never freed: a HIP graph captured at
-            # one batch size keeps pointing at its buffers while other sizes run eagerly
             B = x.shape[0]
-            scratch = self.__dict__.setdefault("_trunk_scratch", {})
-            key = (x.device, B)
-            if key not in scratch:
-                scratch[key] = {"absmax": [torch.zeros(B, dtype=torch.float32, device=x.device)
-                                           for _ in range(2)]}
-            bufs = scratch[key]["absmax"]
+            ent = self._scratch(x.device, B)
+            bufs = ent["absmax"]
             if isinstance(self.stem, _HipStem):
                 h = self.stem(x, absmax=bufs[0])
             else:
@@ -510,10 +532,9 @@ class FusedInferenceNet(nn.Module, Inference):
             splits = self.splitk_for(B)
             if splits and all(c.algo == "wino4" for c in c1s + c2s):
                 n = splits * B * 64 * c1s[0].channels
-                part = scratch[key].get("part")
+                part = ent.get("part")
                 if part is None or part.numel() != n:
-                    part = scratch[key]["part"] = torch.empty(n, dtype=torch.float32,
-                                                              device=x.device)
+                    part = ent["part"] = torch.empty(n, dtype=torch.float32, device=x.device)
                 sk = {"part": part, "splits": splits}
             for c1, c2 in zip(c1s, c2s):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)

@@ -76,6 +76,13 @@ class BatchedArena:
                         e.expand()
                 live = [k for k in live
                         if (self.eng[k].game_info()["status"] == nat.AZ_GAME_ACTIVE).any()]
+        for k in (0, 1):
+            # a skipped expansion (node arena full, or a waiting descent deeper than the
+            # tracked path) makes that search differ from the reference's: never score it
+            n = self.eng[k].counters()["arena_overflows"]
+            if n:
+                raise RuntimeError(f"arena engine {k}: node arena overflowed {n} times; the "
+                                   "searches diverged from the reference (raise node_capacity)")
 
     def play(self, n_matches):
         """Play n_matches (in waves of G) and return (wins_a, wins_b, draws, plies)."""

@@ -56,6 +56,13 @@
 #ifndef AZ_W4_STAMP
 #define AZ_W4_STAMP 0
 #endif
+// 1 (product): weight and input slices through buffer descriptors (wave-uniform chunk/step
+// offsets in soffset, no per-lane 64-bit address arithmetic), transform-row offsets and
+// signs compile-time per group (the group loop's last chunk pair peeled), the input scale
+// folded into the row combination; 0 = the round-2 loop (A/B builds)
+#ifndef AZ_W4_DIET
+#define AZ_W4_DIET 1
+#endif
 // experiment hooks (scripts/build_variants.py builds with bits set; results wrong):
 // 1 = no weight loads in the loop, 2 = no transform / input work in the loop, 4 = no MFMAs,
 // 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads.  Product: 0.
@@ -91,6 +98,24 @@ __device__ unsigned long long g_w4_stamps[1024 * 16];
 #else
 #define W4_STAMP(i) \
   do {              \
+  } while (0)
+#endif
+// experiment builds only (-DAZ_W4_CSTAMP=1): every wave's s_memtime at each chunk's start,
+// before and after its closing barrier, [wg < 256][wave][chunk][3], lane 0's vector store
+#ifndef AZ_W4_CSTAMP
+#define AZ_W4_CSTAMP 0
+#endif
+#if AZ_W4_CSTAMP
+__device__ unsigned long long g_w4_cst[256 * 8 * 32 * 3];
+#define W4C_STAMP(v, i)                                                                     \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (v) < 32)                            \
+      g_w4_cst[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (v)) * 3 + (i)] = t_;          \
+  } while (0)
+#else
+#define W4C_STAMP(v, i) \
+  do {                  \
   } while (0)
 #endif
 
@@ -173,10 +198,10 @@ __device__ __forceinline__ int frexp_exp(float x) {
 // window rows of group k: B^T row k = sa * d_a0 + sb * d_a1 (B^T = [1 0 -1 0; 0 1 1 0;
 // 0 -1 1 0; 0 1 0 -1]); multiplying by +-1 is exact, so this is the transform's own
 // add / subtract
-__device__ __forceinline__ int grp_a0(int k) { return k == 0 ? 0 : 1; }
-__device__ __forceinline__ int grp_a1(int k) { return k == 3 ? 3 : 2; }
-__device__ __forceinline__ float grp_sa(int k) { return k == 2 ? -1.0f : 1.0f; }
-__device__ __forceinline__ float grp_sb(int k) { return (k == 1 || k == 2) ? 1.0f : -1.0f; }
+__host__ __device__ constexpr int grp_a0(int k) { return k == 0 ? 0 : 1; }
+__host__ __device__ constexpr int grp_a1(int k) { return k == 3 ? 3 : 2; }
+__host__ __device__ constexpr float grp_sa(int k) { return k == 2 ? -1.0f : 1.0f; }
+__host__ __device__ constexpr float grp_sb(int k) { return (k == 1 || k == 2) ? 1.0f : -1.0f; }
 
 // weight fragment of linear step q (chunk L = q / 4 = (group k, channel chunk c), point l)
 template <class G>
@@ -186,6 +211,18 @@ __device__ __forceinline__ void load_b(Frag<G>& f, const char* wq, int wlane, in
 #pragma unroll
   for (int pl = 0; pl < G::PLANES; ++pl)
     f.v[pl] = *reinterpret_cast<const Word8<G>*>(step + wlane + pl * G::C * 32);
+}
+
+// the same through the weights' buffer descriptor: the step's byte offset is wave-uniform
+// (soffset), the lane's (wlane) a fixed voffset
+template <class G>
+__device__ __forceinline__ void load_b(Frag<G>& f, __amdgpu_buffer_rsrc_t rw, int wlane, int q) {
+  const int L = q >> 2, l = q & 3, k = L >> 3, c = L & 7;
+  const int so = (c * 16 + 4 * k + l) * G::STEP_BYTES;
+#pragma unroll
+  for (int pl = 0; pl < G::PLANES; ++pl)
+    f.v[pl] = __builtin_bit_cast(
+        Word8<G>, __builtin_amdgcn_raw_buffer_load_b128(rw, wlane, so + pl * G::C * 32, 0));
 }
 
 template <class G>
@@ -228,6 +265,17 @@ __device__ __forceinline__ void load_in(f32x4 (&ld)[G::LD_PER_THREAD], const flo
 #pragma unroll
   for (int j = 0; j < G::LD_PER_THREAD; ++j)
     ld[j] = *reinterpret_cast<const f32x4*>(x + goff[j] + c * 16);
+}
+
+// the same through the input's buffer descriptor (goff in bytes; the chunk's channel offset
+// is wave-uniform)
+template <class G>
+__device__ __forceinline__ void load_in(f32x4 (&ld)[G::LD_PER_THREAD], __amdgpu_buffer_rsrc_t rx,
+                                        const int (&goff)[G::LD_PER_THREAD], int L) {
+  const int c = L & 7;
+#pragma unroll
+  for (int j = 0; j < G::LD_PER_THREAD; ++j)
+    ld[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, goff[j], c * 64, 0));
 }
 
 // ... and into the slot's padded interior
@@ -279,6 +327,29 @@ __device__ __forceinline__ void make_rows(f32x2 (&rk)[4], const char* slot, int 
   f32x2 d[8];
   read_rows<G>(d, slot, rbase, cols, L);
   combine_rows(rk, d, L);
+}
+
+// Compile-time group KK (AZ_W4_DIET): the window rows of slot PAR read with immediate LDS
+// offsets from the lane's four column bases cb[b] (rbase + column slot), and combined with
+// the input scale folded in -- rk = vsc sa d_a0 + vsc sb d_a1 is vsc times the unscaled
+// row exactly (vsc is a power of two), so V and its split are bit-identical to scaling
+// each point afterwards
+template <class G, int KK, int PAR>
+__device__ __forceinline__ void read_rows_k(f32x2 (&d)[8], const char* lds, const int (&cb)[4]) {
+  constexpr int base = G::IN_OFF + PAR * G::IN_SLOT;
+  constexpr int o0 = base + grp_a0(KK) * G::IN_ROW, o1 = base + grp_a1(KK) * G::IN_ROW;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    d[b] = *reinterpret_cast<const f32x2*>(lds + cb[b] + o0);
+    d[4 + b] = *reinterpret_cast<const f32x2*>(lds + cb[b] + o1);
+  }
+}
+
+template <int KK>
+__device__ __forceinline__ void combine_k(f32x2 (&rk)[4], const f32x2 (&d)[8], float vsc) {
+  const f32x2 fa = {grp_sa(KK) * vsc, grp_sa(KK) * vsc}, fb = {grp_sb(KK) * vsc, grp_sb(KK) * vsc};
+#pragma unroll
+  for (int b = 0; b < 4; ++b) rk[b] = __builtin_elementwise_fma(fb, d[4 + b], fa * d[b]);
 }
 
 // V at point (k, l) = (row k of B^T d) B: column combination l
@@ -375,6 +446,8 @@ struct St {
   f32x16 Y[2][2][G::NRT];
   int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], cols[G::TPT], soff[G::TPT], aoff[G::NRT];
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
+  int cbase[G::TPT][4];  // AZ_W4_DIET: the item's window column bases in an input slot
+  __amdgpu_buffer_rsrc_t rx, rw;  // input and weight descriptors (AZ_W4_DIET)
   int wlane, tid, b0, nb;
   int cs;             // first channel chunk of this workgroup's split (0 unless SPLIT)
   int g0;             // its transform-grid row (NG = 1; 0 otherwise)
@@ -432,8 +505,13 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // one chunk L (of parity PAR, so a step's weight ring slot is a compile-time constant): its
 // four steps, the next chunk's transform into the other LDS buffer, the windows of the
 // chunk after that requested
-template <class G, int PAR, int STAGE>
+// KR / KS: the transform-grid rows of chunks v+1 (whose rows are combined here) and v+2
+// (whose windows are read at the end), when known at compile time (AZ_W4_DIET); -1 = from
+// the chunk map at run time
+template <class G, int PAR, int STAGE, int KR = -1, int KS = -1>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
+  constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
+  W4C_STAMP(v, 0);
   const int L = lmap<G>(S, v);
   const char* cur = S.lds + (v & 1) * G::BUF;
   char* nxt = S.lds + ((v + 1) & 1) * G::BUF;
@@ -462,22 +540,37 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
       // chunk L+1's window rows (requested right after the previous barrier) combined
       // behind step 0's MFMAs
 #pragma unroll
-      for (int u = 0; u < G::TPT; ++u) combine_rows(S.rk[u], S.dr[u], Lr);
+      for (int u = 0; u < G::TPT; ++u) {
+        if constexpr (CT)
+          combine_k<KR < 4 ? KR : 3>(S.rk[u], S.dr[u], S.vsc[u]);
+        else
+          combine_rows(S.rk[u], S.dr[u], Lr);
+      }
     }
-    if (!(AZ_W4_EXP & 1))
-      load_b<G>(S.bf[(slot + G::PD) % G::RING], S.wq, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
+    if (!(AZ_W4_EXP & 1)) {
+      if constexpr (AZ_W4_DIET)
+        load_b<G>(S.bf[(slot + G::PD) % G::RING], S.rw, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
+      else
+        load_b<G>(S.bf[(slot + G::PD) % G::RING], S.wq, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
+    }
     // the chunk-after-next's input slice at the chunk's first step: four steps of latency
     // cover before it is stored to LDS at the chunk's end
-    if (l == 0 && !(AZ_W4_EXP & 2)) load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
+    if (l == 0 && !(AZ_W4_EXP & 2)) {
+      if constexpr (AZ_W4_DIET)
+        load_in<G>(S.ld[set_l], S.rx, S.goff, Ll);
+      else
+        load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
+    }
     if constexpr (STAGE >= 0) {
       if (l == 1) res_dma<G, STAGE>(S, L & 7);
     }
 #pragma unroll
     for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
-      if (l == 0) put_point<G, 0>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
-      if (l == 1) put_point<G, 1>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
-      if (l == 2) put_point<G, 2>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
-      if (l == 3) put_point<G, 3>(nxt, S.rk[u], S.soff[u], S.vsc[u]);
+      const float vs = CT ? 1.0f : S.vsc[u];  // CT: the scale is in rk already
+      if (l == 0) put_point<G, 0>(nxt, S.rk[u], S.soff[u], vs);
+      if (l == 1) put_point<G, 1>(nxt, S.rk[u], S.soff[u], vs);
+      if (l == 2) put_point<G, 2>(nxt, S.rk[u], S.soff[u], vs);
+      if (l == 3) put_point<G, 3>(nxt, S.rk[u], S.soff[u], vs);
     }
     if (l < 3) {
 #pragma unroll
@@ -499,12 +592,18 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   }
   // slot (v+2) & 1 = v & 1 held chunk v's input, whose rows were formed in chunk v-1
   if (!(AZ_W4_EXP & 2)) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
+  W4C_STAMP(v, 1);
   if (!(AZ_W4_EXP & 8)) lds_barrier();
+  W4C_STAMP(v, 2);
   read_a<G>(S.af, nxt, 0, S.aoff);
   // the next chunk's window rows (chunk L+2, stored just before the barrier)
 #pragma unroll
-  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
+  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
+    if constexpr (CT)
+      read_rows_k<G, KS < 4 ? KS : 3, PAR>(S.dr[u], S.lds, S.cbase[u]);
+    else
+      read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
+  }
 }
 
 template <class G>
@@ -524,6 +623,18 @@ __device__ __forceinline__ void run_group(St<G>& S) {
   constexpr int KV = G::NG == 4 ? K : 0;  // the group's place in this workgroup's sequence
   if constexpr (G::NC == 1) {
     run_chunk<G, KV & 1, STAGE>(S, KV);  // one chunk per group: the parity alternates by group
+  } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
+    // the whole-K kernel: chunks v = 8K + c; the rows combined in chunk v are chunk v+1's,
+    // the windows read at its end chunk v+2's -- both in group K except in the last pair,
+    // peeled so every group index is a compile-time constant
+    constexpr int KN = K + 1;
+#pragma unroll 1
+    for (int c = 0; c < G::NC - 2; c += 2) {
+      run_chunk<G, 0, STAGE, K, K>(S, KV * G::NC + c);
+      run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + c + 1);
+    }
+    run_chunk<G, 0, STAGE, K, KN>(S, KV * G::NC + G::NC - 2);
+    run_chunk<G, 1, STAGE, KN, KN>(S, KV * G::NC + G::NC - 1);
   } else {
 #pragma unroll 1
     for (int c = 0; c < G::NC; c += 2) {
@@ -585,6 +696,12 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   S.lds = reinterpret_cast<char*>(lds4);
   S.x = x;
   S.wq = wq;
+  if constexpr (AZ_W4_DIET) {
+    const long long xb = (long long)n_boards * 64 * C * 4;
+    S.rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, xb < 0x7fffffff ? (int)xb : 0x7fffffff,
+                                             0x00020000);
+    S.rw = __builtin_amdgcn_make_buffer_rsrc((void*)wq, 0, G::QSTEPS * G::STEP_BYTES, 0x00020000);
+  }
   S.res = res;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -618,6 +735,8 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
 #pragma unroll
     for (int b = 0; b < 4; ++b) S.cols[u] |= col_slot(2 * tx + b) << (8 * b);
     S.soff[u] = T * 32 + (((p >> 2) ^ ((T >> 3) & 1)) << 4) + (p & 3) * 4;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) S.cbase[u][b] = S.rbase[u] + col_slot(2 * tx + b) * 64;
     S.vsc[u] = 1.0f;
     if constexpr (G::SCALED) {
       // |V| <= 4 max |x| < 2^(e+2): scaled by 2^(13-e), the transformed inputs stay below
@@ -637,7 +756,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     const int P = (P0 & ~3) | ((P0 & 1) << 1) | ((P0 >> 1) & 1);
     const int bd = P >> 6, pos = P & 63;
     const int bs = bd < nb ? bd : nb - 1;
-    S.goff[j] = ((b0 + bs) * 64 + pos) * C + 4 * q;
+    S.goff[j] = (((b0 + bs) * 64 + pos) * C + 4 * q) * (AZ_W4_DIET ? 4 : 1);  // DIET: bytes
     S.ldst[j] = bd * G::IN_BOARD + ((pos >> 3) + 1) * G::IN_ROW + col_slot((pos & 7) + 1) * 64 + q * 16;
   }
 
@@ -648,15 +767,28 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
       *reinterpret_cast<f32x4*>(in0 + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 ld0[G::LD_PER_THREAD], ld1[G::LD_PER_THREAD];
-    load_in<G>(ld0, x, S.goff, lmap<G>(S, 0));
-    load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, x, S.goff, lmap<G>(S, 1));
-    if (G::IPD == 2) load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));  // stored at the end of chunk 0
+    if constexpr (AZ_W4_DIET) {
+      load_in<G>(ld0, S.rx, S.goff, lmap<G>(S, 0));
+      load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, S.rx, S.goff, lmap<G>(S, 1));
+      if (G::IPD == 2) load_in<G>(S.ld[0], S.rx, S.goff, lmap<G>(S, 2));
 #pragma unroll
-    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, qmap<G>(S, i));
+      for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], S.rw, S.wlane, qmap<G>(S, i));
+    } else {
+      load_in<G>(ld0, x, S.goff, lmap<G>(S, 0));
+      load_in<G>(G::IPD == 1 ? S.ld[0] : ld1, x, S.goff, lmap<G>(S, 1));
+      if (G::IPD == 2) load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));  // stored at the end of chunk 0
+#pragma unroll
+      for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, qmap<G>(S, i));
+    }
     lds_barrier();  // the zero fill before any interior store
     store_in<G>(in0, ld0, S.ldst);
     store_in<G>(in0 + G::IN_SLOT, G::IPD == 1 ? S.ld[0] : ld1, S.ldst);
-    if (G::IPD == 1) load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));  // stored at the end of chunk 0
+    if (G::IPD == 1) {  // stored at the end of chunk 0
+      if constexpr (AZ_W4_DIET)
+        load_in<G>(S.ld[0], S.rx, S.goff, lmap<G>(S, 2));
+      else
+        load_in<G>(S.ld[0], x, S.goff, lmap<G>(S, 2));
+    }
     lds_barrier();
 #pragma unroll
     for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], S.cols[u], lmap<G>(S, 0));
@@ -891,6 +1023,13 @@ extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const
                         "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4, 8, 16 or 32, got %d",
                         splits);
 }
+
+#if AZ_W4_CSTAMP
+extern "C" int az_w4_cstamps(unsigned long long* host, int n) {
+  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_cst), sizeof(unsigned long long) * n));
+  return AZ_OK;
+}
+#endif
 
 #if AZ_W4_STAMP
 extern "C" int az_w4_stamps(unsigned long long* host, int n) {

@@ -259,7 +259,8 @@ class BatchedSelfPlay:
 
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
-                 device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1):
+                 device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1,
+                 require_graph=False):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -281,6 +282,10 @@ class BatchedSelfPlay:
         else:
             self.net = net.to(self.device).eval()
         self.use_graph = use_graph
+        # require_graph: a failed capture raises instead of running eagerly (bench.py: a
+        # regression must not show up only as lost throughput)
+        self.require_graph = require_graph
+        self.graph_error = None
         self.steps_per_graph = max(1, int(steps_per_graph))
         self.graph = None  # {steps: CUDAGraph}: one replay = that many simulation steps
 
@@ -326,8 +331,13 @@ class BatchedSelfPlay:
             try:
                 self._capture()
             except Exception as ex:  # capture unsupported for this net: run eagerly
+                if self.require_graph:
+                    raise
+                import warnings
+
                 self.use_graph = False
                 self.graph_error = repr(ex)
+                warnings.warn(f"HIP graph capture failed, running the step eagerly: {ex!r}")
         if self.graph is None:
             for _ in range(n):
                 self._step_body()

@@ -8,9 +8,10 @@ Workload (BASELINE.json configs[2], the one the metric is quoted on): 8x8 Othell
 1,024 = 1,024 concurrent games per GPU with one leaf each per step; the reference's
 self-play settings (train.py:399-423): c_puct 2, Dirichlet alpha 1 / eps 0.3 at the root,
 temperature 1 for 35 plies then 0, lambda 0.98.  The net is fp32-accurate: the 3x3 trunk runs
-fp32 operands split into three bf16 words on the 16-bit MFMA pipe with fp32 accumulation
-(error bounded by the fp32 MFMA kernel's, tests/test_nn_gpu.py); --conv-precision fp32
-selects the plain fp32 MFMA kernel.
+fp32 operands as exactly scaled fp16 hi + lo pairs, three fp16 MFMA products with fp32
+accumulation (Winograd F(2x2,3x3), csrc/conv_wino4.hip; error bounded by the fp32 MFMA
+kernel's, tests/test_nn_gpu.py); --conv-precision split3 / fp32 select the bf16x3 and the
+plain fp32 MFMA kernels.
 
 A step is one batched simulation over every game slot: select (descent + leaf pack) ->
 net forward -> expand+backup -> move phase; games restart as they finish (weak scaling:
@@ -35,8 +36,9 @@ Also measured in the same run:
                 (profiles/oth_step_traffic.json), or null.
   cpu_baseline  the oracle's restatement of the reference self-play (oracle/mcts.py:
                 sequential MCTS, batch-1 torch-CPU inference of the same net, the C board
-                oracle) in --cpu-workers single-threaded processes (default 8) for a
-                bounded sample of moves each, games/s summed.
+                oracle) in --cpu-workers single-threaded processes (default: every CPU this
+                job is allotted) for a bounded sample of moves each; the per-core rate times
+                os.cpu_count() is the whole host's.
 """
 import argparse
 import json
@@ -108,8 +110,9 @@ def parse():
                          "records 8-step graphs completely: DESIGN.md section 5)")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--cpu-workers", type=int, default=8,
-                    help="host cores (one single-threaded process each) for cpu_baseline")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="host cores (one single-threaded process each) for cpu_baseline; "
+                         "default: every CPU allotted to this job (host_cpu_share)")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-kernel", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "oth_step_traffic.json"))
@@ -414,40 +417,116 @@ def cpu_model():
     return "unknown"
 
 
+def host_cpu_share():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup-v2 CPU
+    quota (a GPU box shows the whole machine in os.cpu_count() but allots a job a share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def calibration_for(cal, net_kind, sims, model, n_cpus):
+    """The reference/port ratio of profiles/cpu_calibration.json, applicable only to the
+    same net and sims on the same CPU model with the same CPU count it was measured on (the
+    gap between the reference's threaded Python search and the port depends on the CPU)."""
+    if not cal or cal.get("net") != net_kind or cal.get("sims") != sims:
+        return None
+    if cal.get("cpu_model") != model or cal.get("os_cpu_count") != n_cpus:
+        return None
+    return cal.get("ratio_reference_over_port")
+
+
 def cpu_baseline_pool(net_kind, sims, seconds, workers):
-    """cpu_baseline on `workers` host cores at once, one process each (started before any
-    GPU work of theirs could exist: they hide the GPUs), like the reference's spawn-pool
-    self-play workers (train.py:220-222); worker w samples the game from ply w*60/workers,
-    so the moves cover the whole game; games/s summed over the workers.  `value` is that
-    rate times the calibration ratio measured in the build container (reference pool /
-    port on the same cores, full games: profiles/cpu_calibration.json), i.e. the port's
-    rate expressed as the reference's."""
+    """cpu_baseline on `workers` host cores at once, one single-threaded process each
+    (started before any GPU work of theirs could exist: they hide the GPUs), like the
+    reference's spawn-pool self-play workers (train.py:210-222, one per host core); worker w
+    samples the game from ply w*60/workers, so the moves cover the whole game.  Games are
+    independent processes, so the host's rate is the per-core rate x os.cpu_count()
+    (BASELINE.md section 3): `value` with `cores` = os.cpu_count(), the measured cores beside
+    it.  The calibration ratio (reference pool / port, full games) scales `value` only on
+    the CPU model and count it was measured on; elsewhere it is reported, not applied."""
     outs = _cpu_pool(net_kind, sims, seconds, workers)
     moves = sum(o["moves"] for o in outs)
-    port = float(sum(o["games_per_s"] for o in outs))
-    ratio = None
-    if os.path.exists(CALIBRATION_JSON):
-        cal = json.load(open(CALIBRATION_JSON))
-        if cal.get("net") == net_kind and cal.get("sims") == sims:
-            ratio = cal.get("ratio_reference_over_port")
+    port = float(sum(o["games_per_s"] for o in outs))  # the measured cores together
+    per_core = port / workers
+    n_host = os.cpu_count() or workers
+    model = cpu_model()
+    cal = json.load(open(CALIBRATION_JSON)) if os.path.exists(CALIBRATION_JSON) else None
+    ratio = calibration_for(cal, net_kind, sims, model, n_host)
+    host = per_core * n_host
     net_name = "AlphaZeroNet(5,128)" if net_kind == "az5x128" else "FastOthelloNet"
-    return {"value": port * ratio if ratio else port, "unit": "games/s",
-            "cores": workers, "kind": "port",
-            "calibration_ratio": ratio, "port_value": port,
-            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
-            "sample": f"{workers} single-threaded worker processes; worker w plays from ply "
-                      f"w*{int(REF_PLIES_PER_GAME)}/{workers} (seeded random opening) for "
-                      f"{seconds:.0f} s of {sims}-sim moves ({moves} moves in all); "
-                      f"{net_name} fp32 batch-1 torch-CPU, oracle/mcts.py SeqMCTS; per worker "
-                      f"games/s = 1/(s_per_move x {REF_PLIES_PER_GAME:.0f} plies), summed; "
-                      + (f"value = port x calibration_ratio {ratio:.3f} (reference pool / port, "
-                         "full games, same 8 cores: profiles/cpu_calibration.json)" if ratio
-                         else "uncalibrated"),
+    cal_note = None
+    if cal:
+        cal_note = {"ratio_reference_over_port": cal.get("ratio_reference_over_port"),
+                    "cpu_model": cal.get("cpu_model"), "os_cpu_count": cal.get("os_cpu_count"),
+                    "games_per_side": (cal.get("reference") or {}).get("games"),
+                    "applied": ratio is not None}
+    return {"value": host * ratio if ratio else host, "unit": "games/s",
+            "cores": n_host, "kind": "port", "cores_measured": workers,
+            "per_core_games_per_s": per_core, "measured_cores_games_per_s": port,
+            "calibration_ratio": ratio, "calibration": cal_note,
+            "cpu_model": model, "os_cpu_count": n_host,
+            "sample": f"{workers} single-threaded worker processes (the CPUs allotted to this "
+                      f"job) at once; worker w plays from ply w*{int(REF_PLIES_PER_GAME)}/"
+                      f"{workers} (seeded random opening) for {seconds:.0f} s of {sims}-sim "
+                      f"moves ({moves} moves in all); {net_name} fp32 batch-1 torch-CPU, "
+                      f"oracle/mcts.py SeqMCTS; per worker games/s = 1/(s_per_move x "
+                      f"{REF_PLIES_PER_GAME:.0f} plies); value = mean per-core rate x "
+                      f"os.cpu_count() = {n_host} (independent game processes scale by core; "
+                      "on an SMT host this overstates the CPU)"
+                      + (f" x calibration_ratio {ratio:.3f}" if ratio else
+                         "; uncalibrated: the calibration's CPU differs, and the port is faster "
+                         "than the reference there (ratio < 1), so this overstates the CPU"),
             "per_worker_games_per_s": [round(o["games_per_s"], 5) for o in outs]}
+
+
+STAT_KEYS = ("moves", "games_done", "sims", "plies_total", "games_total", "window_s")
+
+
+def gather_stats(stats, dist, world):
+    """Every rank's window statistics (a float64 vector in STAT_KEYS order) as a
+    [world, 6] array on every rank (one all_gather; a plain copy at world 1)."""
+    if dist is None:
+        return stats.cpu().numpy()[None]
+    allst = [torch.zeros_like(stats) for _ in range(world)]
+    dist.all_gather(allst, stats)
+    return torch.stack(allst).cpu().numpy()
+
+
+def aggregate_stats(allst, sims_per_move):
+    """Whole-job figures from gather_stats' rows: counts summed over ranks, the window =
+    the slowest rank's (max over ranks), plies per game from every rank's completed games
+    (the reference's 60 until 16 exist).  Every slot always has a game in progress and runs
+    one simulation per step; a move is exactly `sims` simulations, so games/s =
+    simulations/s / (sims x plies per game).  (Game completions inside the window follow the
+    start schedule of the first game generation rather than the steady state, so they are
+    reported, not used.)"""
+    allst = np.asarray(allst, np.float64).reshape(-1, len(STAT_KEYS))
+    tot = allst.sum(0)
+    t_max = float(allst[:, 5].max())
+    gtot = tot[4]
+    plies_per_game = float(tot[3] / gtot) if gtot >= 16 else REF_PLIES_PER_GAME
+    return {"value": float(tot[2] / sims_per_move / plies_per_game / t_max),
+            "moves": float(tot[0]), "games_done": float(tot[1]), "sims": float(tot[2]),
+            "plies_per_game": plies_per_game, "window_s": t_max,
+            "per_rank": [{"sims": int(r[2]), "moves": int(r[0]), "window_s": round(float(r[5]), 4)}
+                         for r in allst]}
 
 
 def main():
     a = parse()
+    if os.environ.get("AZ_FAULTHANDLER"):  # diagnostics: every thread's Python stack on a fault
+        import faulthandler
+
+        faulthandler.enable(all_threads=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -473,11 +552,15 @@ def main():
     net = make_net(a.net)
     args = dict(SELFPLAY_ARGS, num_simulations=a.sims)
     sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
-                         use_graph=not a.no_graph, device=device, d4_augment=a.d4,
+                         use_graph=not a.no_graph, require_graph=not a.no_graph,
+                         device=device, d4_augment=a.d4,
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
                          sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
                          precision=a.conv_precision, leaves_per_step=a.leaves)
     e = sp.engine
+    if os.environ.get("AZ_DUMP_MAPS"):  # diagnostics: the address map, to place a fault's PC
+        with open("/proc/self/maps") as f_in, open(os.environ["AZ_DUMP_MAPS"], "w") as f_out:
+            f_out.write(f_in.read())
     # stagger slot starts over one game length: at the end of the warmup every slot plays
     # and the game phases are uniform (steady state of continuous self-play)
     stagger = (-(-a.sims // a.leaves) + 1) * int(REF_PLIES_PER_GAME)
@@ -522,21 +605,10 @@ def main():
     games_total = c1["games_finished"]
     stats = torch.tensor([moves, games_done, sims, plies_total, games_total, dt],
                          dtype=torch.float64, device=coll_device)
-    if dist is not None:
-        allst = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(allst, stats)
-        allst = torch.stack(allst).cpu().numpy()
-    else:
-        allst = stats.cpu().numpy()[None]
-    moves_all, games_all, sims_all = allst[:, 0].sum(), allst[:, 1].sum(), allst[:, 2].sum()
-    plies_all, gtot_all = allst[:, 3].sum(), allst[:, 4].sum()
-    t_max = float(allst[:, 5].max())
-    plies_per_game = plies_all / gtot_all if gtot_all >= 16 else REF_PLIES_PER_GAME
-    # Every slot always has a game in progress and runs one simulation per step; a move is
-    # exactly `sims` simulations, so games/s = simulations/s / (sims x plies per game).
-    # (Game completions inside the window follow the start schedule of the first game
-    # generation rather than the steady state, so they are reported, not used.)
-    value = sims_all / a.sims / plies_per_game / t_max
+    allst = gather_stats(stats, dist, world)
+    agg = aggregate_stats(allst, a.sims)
+    t_max, plies_per_game, value = agg["window_s"], agg["plies_per_game"], agg["value"]
+    moves_all, games_all, sims_all = agg["moves"], agg["games_done"], agg["sims"]
     basis = ("simulations in the window / (sims per move x mean plies per completed game) / "
              "window seconds (all ranks)")
 
@@ -561,7 +633,7 @@ def main():
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
                    "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
-                   "hip_graph": sp.graph is not None},
+                   "hip_graph": sp.graph is not None, "graph_error": sp.graph_error},
         "value_basis": basis,
         "detail": {"moves": int(moves_all),
                    "moves_based_games_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),
@@ -571,6 +643,11 @@ def main():
                    "arena_overflows": int(c1["arena_overflows"]),
                    "samples_dropped": int(c1["samples_dropped"])},
     }
+    if dist is not None:
+        # what the process group actually was, and every rank's share (a SCALE line shows
+        # by itself that N ranks ran and how value was formed)
+        result["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                          "per_rank": agg["per_rank"]}
     if kb is not None:
         ms, n = ms_step_kernel, a.kernel_n
         ms_hot = kb.time_ms()
@@ -598,7 +675,8 @@ def main():
             and getattr(sp.net, "conv_impl", "") == "hip":
         result["roofline_conv"] = conv_roofline(sp, device, a.games * a.leaves)
     if rank == 0 and not a.skip_cpu:
-        result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds, a.cpu_workers)
+        result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds,
+                                                   a.cpu_workers or host_cpu_share())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

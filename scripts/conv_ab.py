@@ -41,6 +41,7 @@ def main():
             nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(t), C, mode, nat.stream_ptr()), "prep")
             wq[("direct", mname)] = t
     for B in batches:
+        torch.manual_seed(B)  # the same inputs in every run (y_sha compares builds)
         x = torch.randn(B, C, 8, 8, device=dev).relu().contiguous(memory_format=torch.channels_last)
         r = torch.randn_like(x).relu().contiguous(memory_format=torch.channels_last)
         amax = board_absmax(x)
@@ -80,6 +81,9 @@ def main():
                 e1.record()
             torch.cuda.synchronize()
             ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
+            import hashlib
+
+            y_sha = hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest()[:16]
             if not with_res:
                 y = y + r  # compare the residual-free form on the same footing (ReLU aside)
             if base is None:
@@ -88,7 +92,8 @@ def main():
             print(json.dumps({"kernel": name, "mode": mname, "boards": B, "residual": with_res,
                               "avg_launch_us": round(ms * 1e3, 2),
                               "algorithmic_tflops": round(flop / (ms * 1e-3) / 1e12, 1),
-                              "max_abs_diff_vs_first": float((y - base).abs().max())}),
+                              "max_abs_diff_vs_first": float((y - base).abs().max()),
+                              "y_sha": y_sha, "lib": os.environ.get("AZ_LIB_PATH", "product")}),
                   flush=True)
 
 

@@ -81,3 +81,45 @@ def _play(bot_player, sims, seed):
 def test_interactive_caller_loop_matches_reference(bot_player, seed):
     plies, bot_moves = _play(bot_player, sims=24, seed=seed)
     assert plies >= 30 and bot_moves >= 15
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_dropin_net_search_graph_replay_equals_eager(threads, monkeypatch):
+    """The path real callers take with a Models.py net (train.py's pool, eval.py): the
+    drop-in MCTS evaluates on the fused HIP inference copy and runs each search as replays
+    of one captured select -> net -> expand graph, ceil(sims / K) + 1 of them.  The same
+    searches run eagerly (no graph) must give identical root visit counts and root values
+    over several plies of tree reuse, so the captured graph is replayed on later searches
+    with the engine's current buffers."""
+    import torch
+
+    from MCTS_model import _EngineSearch
+    from Models import AlphaZeroNet
+
+    def run(use_graph):
+        monkeypatch.setattr(_EngineSearch, "use_graph", use_graph)
+        torch.manual_seed(0)
+        net = AlphaZeroNet(8, 65, 5, 128)
+        env = OthelloGameNew(8)
+        mcts = MCTS(env, {"c_puct": 2.0, "num_simulations": 48, "num_threads": threads}, net,
+                    dirichlet_alpha=1.0, dirichlet_epsilon=0.3)
+        state, player = env.get_initial_state(), 1
+        out = []
+        for ply in range(6):
+            np.random.seed(100 + ply)
+            probs = mcts.policy_improve_step(state, player, temp=1.0)
+            counts = np.array([c.visit_count if c else 0 for c in
+                               (mcts.root.children.get(a) for a in range(65))])
+            out.append((counts, mcts.root.value, mcts.root.visit_count, probs))
+            action = int(np.flatnonzero(counts == counts.max())[0])
+            mcts.make_move(action)
+            state = env.get_next_state(state, action, player)
+            player = -player
+        assert (getattr(mcts._impl, "_graph", None) is not None) == use_graph
+        return out
+
+    g, e = run(True), run(False)
+    for ply, (a, b) in enumerate(zip(g, e)):
+        assert np.array_equal(a[0], b[0]), ply
+        assert a[1] == b[1] and a[2] == b[2], ply
+        assert np.array_equal(a[3], b[3]), ply

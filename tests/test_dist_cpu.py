@@ -90,3 +90,62 @@ def test_pack_unpack_rows_edge_counts():
         assert np.array_equal(got["pi"].numpy(), s["pi"])
         assert np.array_equal(got["z"].numpy(), s["z"])
         assert np.array_equal(got["player"].numpy(), s["player"])
+
+
+def _bench_stats_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # [moves, games_done, sims, plies_total, games_total, window_s] of this rank
+    mine = [[10, 1, 4000, 600, 10, 2.0], [12, 2, 4800, 1260, 20, 2.5]][rank]
+    allst = bench.gather_stats(torch.tensor(mine, dtype=torch.float64), dist, world)
+    agg = bench.aggregate_stats(allst, 400)
+    q.put((rank, agg, dist.get_backend(), dist.get_world_size()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_stats_aggregation_world2():
+    """bench.py's whole-job value over a world-2 gloo group: counts summed over ranks, the
+    slowest rank's window, plies per game over every rank's completed games."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_stats_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    want_ppg = (600 + 1260) / (10 + 20)
+    want = (4000 + 4800) / 400 / want_ppg / 2.5
+    for rank, agg, backend, world in res:
+        assert backend == "gloo" and world == 2
+        assert agg["sims"] == 8800 and agg["moves"] == 22 and agg["window_s"] == 2.5
+        assert agg["plies_per_game"] == want_ppg
+        assert abs(agg["value"] - want) < 1e-12
+        assert [r["sims"] for r in agg["per_rank"]] == [4000, 4800]
+        assert [r["window_s"] for r in agg["per_rank"]] == [2.0, 2.5]
+
+
+def test_bench_stats_fallback_plies_and_cpu_calibration_gate():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    # fewer than 16 completed games: the reference's 60 plies per game
+    agg = bench.aggregate_stats(np.array([[5, 0, 1000, 100, 2, 1.0]]), 100)
+    assert agg["plies_per_game"] == bench.REF_PLIES_PER_GAME
+    assert abs(agg["value"] - 1000 / 100 / 60 / 1.0) < 1e-12
+    cal = {"net": "az5x128", "sims": 400, "cpu_model": "X", "os_cpu_count": 8,
+           "ratio_reference_over_port": 0.5}
+    assert bench.calibration_for(cal, "az5x128", 400, "X", 8) == 0.5
+    assert bench.calibration_for(cal, "az5x128", 400, "Y", 8) is None   # other CPU model
+    assert bench.calibration_for(cal, "az5x128", 400, "X", 256) is None  # other CPU count
+    assert bench.calibration_for(cal, "fast", 400, "X", 8) is None
+    assert 1 <= bench.host_cpu_share() <= (os.cpu_count() or 1)
