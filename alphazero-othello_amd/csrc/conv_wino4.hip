@@ -100,6 +100,25 @@ __device__ unsigned long long g_w4_stamps[1024 * 16];
   do {              \
   } while (0)
 #endif
+// experiment builds only (-DAZ_W4_CSTAMP=1, scripts/w4_chunk_stamps.py): every wave's
+// s_memtime at each chunk's start, before and after its closing barrier, [wg < 256][wave]
+// [chunk][3], lane 0's vector store
+#ifndef AZ_W4_CSTAMP
+#define AZ_W4_CSTAMP 0
+#endif
+#if AZ_W4_CSTAMP
+__device__ unsigned long long g_w4_cst[256 * 8 * 32 * 3];
+#define W4C_STAMP(v, i)                                                                     \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (v) < 32)                            \
+      g_w4_cst[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (v)) * 3 + (i)] = t_;          \
+  } while (0)
+#else
+#define W4C_STAMP(v, i) \
+  do {                  \
+  } while (0)
+#endif
 // experiment builds only (-DAZ_W4_CSTAMP=1): every wave's s_memtime at each chunk's start,
 // before and after its closing barrier, [wg < 256][wave][chunk][3], lane 0's vector store
 #ifndef AZ_W4_CSTAMP
@@ -511,6 +530,7 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 template <class G, int PAR, int STAGE, int KR = -1, int KS = -1>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
+  W4C_STAMP(v, 0);
   W4C_STAMP(v, 0);
   const int L = lmap<G>(S, v);
   const char* cur = S.lds + (v & 1) * G::BUF;
@@ -1023,6 +1043,13 @@ extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const
                         "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4, 8, 16 or 32, got %d",
                         splits);
 }
+
+#if AZ_W4_CSTAMP
+extern "C" int az_w4_cstamps(unsigned long long* host, int n) {
+  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_cst), sizeof(unsigned long long) * n));
+  return AZ_OK;
+}
+#endif
 
 #if AZ_W4_CSTAMP
 extern "C" int az_w4_cstamps(unsigned long long* host, int n) {

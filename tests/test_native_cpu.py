@@ -275,3 +275,29 @@ def test_splitk_table_picks_the_measured_fastest_form(monkeypatch):
     assert {b: F.splitk_for(b) for b in want} == want
     monkeypatch.setenv("AZ_SPLITK", "0")
     assert F.splitk_for(4) == 0
+
+
+def test_trunk_scratch_is_bounded_and_pinned_under_capture(monkeypatch):
+    """FusedInferenceNet keeps per-batch-size trunk scratch: sizes seen during a HIP graph
+    capture stay (the graph points at them); other sizes are capped, least recently used
+    dropped first; release_scratch() drops the unpinned ones."""
+    import torch
+
+    from Models import FusedInferenceNet
+
+    class Net:
+        scratch_cap = 2
+
+    net = Net()
+    sc = lambda B: FusedInferenceNet._scratch(net, torch.device("cpu"), B)  # noqa: E731
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    pinned = sc(1024)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    for B in range(1, 40):
+        sc(B)
+    keys = [k[1] for k in net._trunk_scratch]
+    assert 1024 in keys and len(keys) == 1 + net.scratch_cap
+    assert keys[-2:] == [38, 39]  # the most recent eager sizes
+    assert sc(1024) is pinned and pinned["pinned"]
+    FusedInferenceNet.release_scratch(net)
+    assert [k[1] for k in net._trunk_scratch] == [1024]
