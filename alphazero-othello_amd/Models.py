@@ -325,6 +325,22 @@ class _HipConv3x3(nn.Module):
             nat.check(rc, name)
         return y
 
+    def forward_heads(self, x, res, in_absmax, hw, priors, values):
+        """This conv (the trunk's last: residual + ReLU, fp16x2 Winograd) with AlphaZeroNet's
+        heads fused into its epilogue (az_conv3x3_wino4_heads_gpu): priors float32 [B, 65]
+        and values float32 [B] written directly, the trunk output never stored."""
+        import az_native as nat
+
+        assert self.algo == "wino4" and self.precision == "fp16x2"
+        x = x.contiguous(memory_format=torch.channels_last)
+        res = res.contiguous(memory_format=torch.channels_last)
+        nat.check(nat.lib.az_conv3x3_wino4_heads_gpu(
+            nat.ptr(x), nat.ptr(self.wq), nat.ptr(self.bias), nat.ptr(res), x.shape[0],
+            self.channels, self.mode, nat.ptr(in_absmax), nat.ptr(hw["wpv"]), nat.ptr(hw["bpv"]),
+            nat.ptr(hw["wpolT"]), nat.ptr(hw["bpol"]), nat.ptr(hw["w1T"]), nat.ptr(hw["b1"]),
+            nat.ptr(hw["w2"]), nat.ptr(hw["b2"]), nat.ptr(priors), nat.ptr(values),
+            nat.stream_ptr()), "az_conv3x3_wino4_heads_gpu")
+
     def forward_stem(self, planes, stem, role, x=None):
         """This conv fused with the stem (`_HipStem`): role 1 = input stem(planes), role 2 =
         residual stem(planes) (input x); bias + ReLU epilogue (csrc/conv16.hip)."""
@@ -491,7 +507,15 @@ class FusedInferenceNet(nn.Module, Inference):
         for k in [k for k, v in sc.items() if not v["pinned"]]:
             del sc[k]
 
-    def _trunk(self, x):
+    # AlphaZeroNet on the fp16x2 Winograd trunk: the heads run in the last conv's epilogue
+    # (az_conv3x3_wino4_heads_gpu, bit-identical to the separate heads kernel; one launch and
+    # the trunk output's HBM round trip fewer per evaluation).  AZ_FUSE_HEADS=0 turns it off.
+    fuse_heads = os.environ.get("AZ_FUSE_HEADS", "1") != "0"
+
+    def _trunk(self, x, heads_into=None):
+        """The trunk's output (NHWC [B, C, 8, 8]); with heads_into = (priors, values) the
+        heads may be fused into the last conv, which then writes them and None is returned
+        (evaluate_into falls back to the separate heads kernel on a tensor)."""
         if x.dim() == 3:
             x = x.unsqueeze(1)
         x = x.contiguous(memory_format=torch.channels_last)
@@ -536,8 +560,14 @@ class FusedInferenceNet(nn.Module, Inference):
                 if part is None or part.numel() != n:
                     part = ent["part"] = torch.empty(n, dtype=torch.float32, device=x.device)
                 sk = {"part": part, "splits": splits}
-            for c1, c2 in zip(c1s, c2s):
+            fuse = (heads_into is not None and not sk and self.fuse_heads
+                    and self._fused_heads_ready() and c2s[-1].algo == "wino4"
+                    and c2s[-1].precision == "fp16x2" and c2s[-1].channels == 128)
+            for i, (c1, c2) in enumerate(zip(c1s, c2s)):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)
+                if fuse and i == len(c1s) - 1:
+                    c2.forward_heads(t, h, bufs[1], self._hw, *heads_into)
+                    return None
                 h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0], **sk)
             return h
         else:
@@ -577,7 +607,9 @@ class FusedInferenceNet(nn.Module, Inference):
         import az_native as nat
 
         B = planes.shape[0]
-        h = self._trunk(planes.view(B, 1, 8, 8))
+        h = self._trunk(planes.view(B, 1, 8, 8), heads_into=(priors, values))
+        if h is None:  # the heads ran in the last conv's epilogue
+            return
         hw = self._hw
         nat.check(nat.lib.az_heads_az_gpu(
             nat.ptr(h), nat.ptr(hw["wpv"]), nat.ptr(hw["bpv"]), nat.ptr(hw["wpolT"]),

@@ -20,7 +20,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/board.hip", "csrc/engine.hip", "csrc/nn_fused.hip", "csrc/conv.hip",
            "csrc/conv16.hip", "csrc/conv_wino.hip", "csrc/conv_wino4.hip", "csrc/heads.hip",
            "csrc/replay.hip"]
-HEADERS = ["csrc/bitboard.h", "csrc/common.h", "csrc/philox.h", "../include/az_othello.h"]
+HEADERS = ["csrc/bitboard.h", "csrc/common.h", "csrc/philox.h", "csrc/heads_az.h",
+           "../include/az_othello.h"]
 OUT = os.path.join(HERE, "libaz_othello.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function"]

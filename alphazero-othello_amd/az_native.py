@@ -117,6 +117,7 @@ SIGNATURES = {
     "az_conv3x3_wino4_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P],
     "az_conv3x3_wino4_splitk_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P,
                                     _I32, _P],
+    "az_conv3x3_wino4_heads_gpu": [_P, _P, _P, _P, _I32, _I32, _I32] + [_P] * 11 + [_P],
     "az_board_absmax_gpu": [_P, _I32, _I32, _P, _P],
     "az_conv3x3_wino_prep_bytes": [_I32, _I32],
     "az_trunk_wino_gpu": [_P] * 7 + [_I32] * 4 + [_P],

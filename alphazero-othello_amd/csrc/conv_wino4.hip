@@ -39,6 +39,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "heads_az.h"
 
 #ifndef AZ_W4_IPD3
 #define AZ_W4_IPD3 1
@@ -677,7 +678,7 @@ struct Epi {
 // output half I (rows 2ty + I): accumulator element e of row tile rt = tile 32rt + (e&3) +
 // 8(e>>2) + 4h, column co; Y[I][j] = output (2ty + I, 2tx + j); + bias (+ the staged
 // residual), ReLU, store, and the boards' max |y|
-template <class G, int I, bool RES, bool RELU>
+template <class G, int I, bool RES, bool RELU, bool HEADS = false>
 __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __restrict__ res,
                                          float* __restrict__ y, int rt0, int h) {
   constexpr int C = G::C;
@@ -698,17 +699,72 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
         else if (RES)
           v += res[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co];
         if (RELU) v = fmaxf(v, 0.0f);
-        y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
-        E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fabsf(v));
+        if constexpr (HEADS) {  // kept for the fused heads (heads_epilogue), not stored
+          S.Y[I][j][t][e] = v;
+        } else {
+          y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
+          E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fabsf(v));
+        }
       }
     }
 }
 
-template <class G, bool RES, bool RELU>
+// The heads' inputs and outputs (az_conv3x3_wino4_heads_gpu); unused otherwise.
+struct HeadsOut {
+  azh::Weights w;
+  float* priors;
+  float* values;
+};
+
+// Last trunk conv with AlphaZeroNet's heads fused (HEADS): both output halves, final
+// (bias, residual, ReLU) in the Y registers, go to an LDS image of the four boards
+// [board][square][C] fp32 (128 KiB over the loop's buffers, free after the barrier), and
+// waves 0-3 run the heads on it (heads_az.h: the same code and registers as the stand-alone
+// heads kernel on the same values, so priors and values are bit-identical to that path)
+// while the trunk output never goes to global memory.
+template <class G>
+__device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int rt0, int h,
+                                               int co) {
+  constexpr int C = G::C;
+  static_assert(G::BOARDS == azh::kBoards && G::THREADS >= 64 * azh::kBoards, "heads layout");
+  static_assert(4 * 64 * C * 4 + 3 * 1024 <= G::LDS_BYTES, "heads LDS");
+  float* img = reinterpret_cast<float*>(S.lds);
+  __syncthreads();  // every wave is past its loop and its staged-residual reads
+#pragma unroll
+  for (int t = 0; t < G::NRT; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int T = 32 * (rt0 + t) + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
+      if (bd >= S.nb) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          img[(bd * 64 + (2 * ty + i) * 8 + 2 * tx + j) * C + co] = S.Y[i][j][t][e];
+    }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool active = wave < azh::kBoards, live = active && wave < S.nb;
+  // a missing board (last workgroup) reads board 0's row: computed, never stored
+  const float4* hp =
+      reinterpret_cast<const float4*>(img + ((live ? wave : 0) * 64 + lane) * C);
+  // p / v after the image (written while other waves still read it); the partial sums
+  // over the image's start (written after heads_four's first barrier)
+  char* base = S.lds;
+  const azh::Scratch L{reinterpret_cast<float(*)[128]>(base + 4 * 64 * C * 4),
+                       reinterpret_cast<float(*)[64]>(base + 4 * 64 * C * 4 + 2048),
+                       reinterpret_cast<float(*)[azh::kBoards][65]>(base),
+                       reinterpret_cast<float4(*)[azh::kBoards][64]>(base + 4352)};
+  azh::heads_four<C>([&](int c) { return hp[c]; }, lane, wave & (azh::kBoards - 1), S.b0 + wave,
+                     live, active, ho.w, L, ho.priors, ho.values);
+}
+
+template <class G, bool RES, bool RELU, bool HEADS = false>
 __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
-    float* __restrict__ in_absmax, float* __restrict__ out_absmax) {
+    float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho) {
   constexpr int C = G::C;
   extern __shared__ float4 lds4[];
   W4_STAMP(0);
@@ -878,12 +934,18 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   run_group<G, 2, STAGED ? 0 : -1>(S);
   W4_STAMP(4);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
-  epilogue<G, 0, RES, RELU>(S, E, res, y, rt0, h);
+  epilogue<G, 0, RES, RELU, HEADS>(S, E, res, y, rt0, h);
   if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
   run_group<G, 3, STAGED ? 1 : -1>(S);
   W4_STAMP(5);
   if (STAGED) vm_barrier();
-  epilogue<G, 1, RES, RELU>(S, E, res, y, rt0, h);
+  epilogue<G, 1, RES, RELU, HEADS>(S, E, res, y, rt0, h);
+  if constexpr (HEADS) {
+    // in_absmax is consumed (every thread read its entries in the prologue)
+    if (threadIdx.x < G::BOARDS && (int)threadIdx.x < nb) in_absmax[b0 + threadIdx.x] = 0.0f;
+    heads_epilogue<G>(S, ho, rt0, h, E.co);
+    return;
+  }
   if (out_absmax) {  // the next layer's in_absmax: one atomic per (wave, board)
 #pragma unroll
     for (int i = 0; i < 2 * G::NRT; ++i) {
@@ -921,13 +983,13 @@ int launch_wino4(const float* x, const void* wq, const float* bias, const float*
   const dim3 blk(G::THREADS);
   const size_t lds = G::LDS_BYTES;
   if (res && relu)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax, HeadsOut{});
   else if (res)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, true, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax, HeadsOut{});
   else if (relu)
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, true>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax, HeadsOut{});
   else
-    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax);
+    hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), dim3(grid), blk, lds, s, x, w, bias, res, y, n_boards, in_absmax, out_absmax, HeadsOut{});
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
@@ -995,7 +1057,7 @@ int launch_wino4_splitk(const float* x, const void* wq, const float* bias, const
   const dim3 grid((unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS), splits);
   hipLaunchKernelGGL((k_conv3x3_wino4<G, false, false>), grid, dim3(G::THREADS),
                      (size_t)G::LDS_BYTES, s, x, static_cast<const char*>(wq), bias, nullptr,
-                     part, n_boards, in_absmax, nullptr);
+                     part, n_boards, in_absmax, nullptr, HeadsOut{});
   AZ_HIP(hipGetLastError());
   const dim3 cg((unsigned)n_boards * (64 * 128 / 4 / 256));
   if (res && relu)
@@ -1064,6 +1126,42 @@ extern "C" int az_w4_stamps(unsigned long long* host, int n) {
   return AZ_OK;
 }
 #endif
+
+extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const float* bias,
+                                          const float* res, int32_t n_boards,
+                                          int32_t channels, int32_t mode, float* in_absmax,
+                                          const float* wpv, const float* bpv,
+                                          const float* wpolT, const float* bpol,
+                                          const float* w1T, const float* b1, const float* w2,
+                                          const float* b2, float* priors, float* values,
+                                          void* stream) {
+  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_heads_gpu: n_boards < 0");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(x && wq && bias && res && in_absmax && wpv && bpv && wpolT && bpol && w1T && b1 &&
+                 w2 && b2 && priors && values,
+             AZ_ERR_ARG, "az_conv3x3_wino4_heads_gpu: null buffer");
+  AZ_REQUIRE(((uintptr_t)x | (uintptr_t)wq | (uintptr_t)bias | (uintptr_t)res | (uintptr_t)wpv |
+              (uintptr_t)w1T | (uintptr_t)b1 | (uintptr_t)w2) % 16 == 0,
+             AZ_ERR_ARG, "az_conv3x3_wino4_heads_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(channels == 128 && mode == AZ_CONV_FP16X2, AZ_ERR_ARG,
+             "az_conv3x3_wino4_heads_gpu: 128 channels in FP16X2 mode only (got %d, mode %d)",
+             channels, mode);
+  using G = W4<AZ_CONV_FP16X2, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_conv3x3_wino4<G, true, true, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  const HeadsOut ho{{wpv, bpv, wpolT, bpol, w1T, b1, w2, b2}, priors, values};
+  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true, true>), dim3(grid), dim3(G::THREADS),
+                     (size_t)G::LDS_BYTES, azc::as_stream(stream), x,
+                     static_cast<const char*>(wq), bias, res, nullptr, n_boards, in_absmax,
+                     nullptr, ho);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
 
 extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias,
                                     const float* res, float* y, int32_t n_boards,

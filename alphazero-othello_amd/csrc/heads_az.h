@@ -1,0 +1,149 @@
+// heads_az.h — AlphaZeroNet's policy and value heads for four boards, one wavefront per
+// board, shared by the stand-alone heads kernel (heads.hip, trunk output read from global
+// memory) and the last trunk conv with the heads fused into its epilogue (conv_wino4.hip,
+// trunk output read from LDS).  Both feed the same registers to the same code, so the two
+// paths give bit-identical priors and values.
+//
+// Reference Models.py:164-221 (inference copy, BatchNorm folded into the 1x1 convs):
+//   p = relu(conv1x1_{C->2}(h) + b)            flattened NCHW: p[c*64 + pos]
+//   logits = pol_fc(p)  (128 -> 65)            priors = softmax(logits)  (MCTS_model.py:319)
+//   v = relu(conv1x1_{C->1}(h) + b)            v[pos]
+//   value = tanh(val_fc2(relu(val_fc1(v))))   (64 -> 256 -> 1)
+// Lane = board square for the 1x1 convs.  The FCs are split by INPUT range over the four
+// waves, each computing its quarter for all four boards (pol_fc^T [128][65]: inputs
+// 32w..32w+31; val_fc1^T [64][256]: inputs 16w..16w+15), so every FC weight is read from L2
+// once per four boards; the partial sums meet in LDS and wave b adds them in order for
+// board b.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace azh {
+
+constexpr int kBoards = 4;  // boards (= computing waves) per workgroup
+
+struct Weights {
+  const float* wpv;    // [3][C]: policy ch 0, policy ch 1, value
+  const float* bpv;    // [3]
+  const float* wpolT;  // [128][65]
+  const float* bpol;   // [65]
+  const float* w1T;    // [64][256]
+  const float* b1;     // [256]
+  const float* w2;     // [256]
+  const float* b2;     // [1]
+};
+
+// LDS the four waves exchange partial sums through (3 KiB + 20.3 KiB); `p` / `v` are
+// written while other waves may still be reading their activations, the rest only after
+// the first barrier
+struct Scratch {
+  float (*p)[128];             // [kBoards][128] relu'd policy 1x1 conv, NCHW-flat
+  float (*v)[64];              // [kBoards][64] relu'd value 1x1 conv
+  float (*lp)[kBoards][65];    // [wave][board][logit] partial logits
+  float4 (*hv)[kBoards][64];   // [wave][board][lane] partial val_fc1 hidden units
+};
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+// Wave w of the workgroup (w < kBoards computes; any further waves of a larger workgroup
+// pass active = false and only take part in the two barriers): xf(c) = channels 4c..4c+3
+// of board w's activations at square `lane` (registers loaded up front, or LDS read on
+// demand), b = that board's index, live = it exists.
+template <int C, class XF>
+__device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool live,
+                                           bool active, const Weights& W, const Scratch& L,
+                                           float* __restrict__ priors,
+                                           float* __restrict__ values) {
+  constexpr int KP = 128 / kBoards, KV = 64 / kBoards;  // FC inputs per wave
+  float wpl[KP];
+  float w64 = 0.f;
+  float4 wq[KV];
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) wpl[k] = W.wpolT[(KP * w + k) * 65 + lane];
+    w64 = lane < KP ? W.wpolT[(KP * w + lane) * 65 + 64] : 0.f;
+#pragma unroll
+    for (int i = 0; i < KV; ++i)
+      wq[i] = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
+    // 1x1 convs (policy 2 channels, value 1 channel) at square `lane`
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    const float4* w0 = reinterpret_cast<const float4*>(W.wpv);
+    const float4* w1 = reinterpret_cast<const float4*>(W.wpv + C);
+    const float4* w2v = reinterpret_cast<const float4*>(W.wpv + 2 * C);
+#pragma unroll
+    for (int c = 0; c < C / 4; ++c) {
+      const float4 a = w0[c], q = w1[c], r = w2v[c], xc = xf(c);
+      d0 += xc.x * a.x + xc.y * a.y + xc.z * a.z + xc.w * a.w;
+      d1 += xc.x * q.x + xc.y * q.y + xc.z * q.z + xc.w * q.w;
+      d2 += xc.x * r.x + xc.y * r.y + xc.z * r.z + xc.w * r.w;
+    }
+    L.p[w][lane] = fmaxf(d0 + W.bpv[0], 0.f);
+    L.p[w][64 + lane] = fmaxf(d1 + W.bpv[1], 0.f);
+    L.v[w][lane] = fmaxf(d2 + W.bpv[2], 0.f);
+  }
+  __syncthreads();
+
+  // this wave's input quarter of both FCs, for every board of the workgroup
+  if (active) {
+#pragma unroll
+    for (int bd = 0; bd < kBoards; ++bd) {
+      float la = 0.f;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) la += wpl[k] * L.p[bd][KP * w + k];
+      L.lp[w][bd][lane] = la;
+      const float l64 = wave_sum(lane < KP ? w64 * L.p[bd][KP * w + lane] : 0.f);
+      if (lane == 0) L.lp[w][bd][64] = l64;
+      float4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < KV; ++i) {
+        const float vi = L.v[bd][KV * w + i];
+        acc.x += wq[i].x * vi;
+        acc.y += wq[i].y * vi;
+        acc.z += wq[i].z * vi;
+        acc.w += wq[i].w * vi;
+      }
+      L.hv[w][bd][lane] = acc;
+    }
+  }
+  __syncthreads();
+  if (!active || !live) return;  // whole wave (b is uniform per wave); no barrier follows
+
+  // board w: the quarters added in order, softmax over the 65 logits
+  float la = W.bpol[lane], l64 = W.bpol[64];
+#pragma unroll
+  for (int q = 0; q < kBoards; ++q) {
+    la += L.lp[q][w][lane];
+    l64 += L.lp[q][w][64];
+  }
+  const float m = fmaxf(wave_max(la), l64);
+  const float e = __expf(la - m), e64 = __expf(l64 - m);
+  const float inv = 1.f / (wave_sum(e) + e64);
+  priors[(size_t)b * 65 + lane] = e * inv;
+  if (lane == 0) priors[(size_t)b * 65 + 64] = e64 * inv;
+
+  // value: lane j -> hidden units 4j..4j+3 of val_fc1, then val_fc2 reduced over the wave
+  float4 acc = reinterpret_cast<const float4*>(W.b1)[lane];
+#pragma unroll
+  for (int q = 0; q < kBoards; ++q) {
+    const float4 a = L.hv[q][w][lane];
+    acc.x += a.x;
+    acc.y += a.y;
+    acc.z += a.z;
+    acc.w += a.w;
+  }
+  const float4 o = reinterpret_cast<const float4*>(W.w2)[lane];
+  const float part = fmaxf(acc.x, 0.f) * o.x + fmaxf(acc.y, 0.f) * o.y +
+                     fmaxf(acc.z, 0.f) * o.z + fmaxf(acc.w, 0.f) * o.w;
+  const float val = wave_sum(part) + W.b2[0];
+  if (lane == 0) values[b] = tanhf(val);
+}
+
+}  // namespace azh

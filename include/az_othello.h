@@ -347,6 +347,20 @@ int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias, cons
                          float* y, int32_t n_boards, int32_t channels, int32_t relu,
                          int32_t mode, float* in_absmax, float* out_absmax, void* stream);
 
+/* The LAST trunk conv (residual + ReLU) of an AlphaZeroNet in FP16X2 mode with the policy and
+ * value heads fused into its epilogue: the trunk output stays in LDS and the workgroup's
+ * four boards run az_heads_az_gpu's computation on it (csrc/heads_az.h, the same code on the
+ * same values: priors and values bit-identical to az_conv3x3_wino4_gpu followed by
+ * az_heads_az_gpu).  Same conv arguments as az_conv3x3_wino4_gpu without y / out_absmax
+ * (in_absmax consumed); heads weights, priors and values as az_heads_az_gpu.  Replaces the
+ * reference's last ResidualBlock conv2 + both heads (Models.py:72-90, 196-221). */
+int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const float* bias,
+                               const float* res, int32_t n_boards, int32_t channels,
+                               int32_t mode, float* in_absmax, const float* wpv,
+                               const float* bpv, const float* wpolT, const float* bpol,
+                               const float* w1T, const float* b1, const float* w2,
+                               const float* b2, float* priors, float* values, void* stream);
+
 /* az_conv3x3_wino4_gpu (FP16X2, 128 channels) for small batches -- a search's few leaves per
  * step, where one workgroup per four boards leaves the chip idle: the 128 input channels are
  * split over 2, 4 or 8 workgroups per board group (splits = 16 or 32 also split the four

@@ -394,3 +394,34 @@ def test_trunk_kernel_is_bit_identical(kind):
         b = fused._trunk(x)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [257, 1024, 1030, 4096])
+def test_fused_heads_bit_identical_to_separate_heads(B, monkeypatch):
+    """AlphaZeroNet on the fp16x2 trunk: the heads fused into the last conv's epilogue
+    (az_conv3x3_wino4_heads_gpu, the trunk output kept in LDS) give the same priors and
+    values, bit for bit, as the last conv followed by the separate heads kernel
+    (az_heads_az_gpu): heads_az.h runs the same code on the same fp32 values.  Ragged
+    batches (a partial last workgroup) included."""
+    from Models import FusedInferenceNet
+
+    torch.manual_seed(3)
+    net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    assert fused.precision == "fp16x2"
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    out = {}
+    for flag in (True, False):
+        monkeypatch.setattr(FusedInferenceNet, "fuse_heads", flag)
+        pr = torch.full((B, 65), float("nan"), device="cuda")
+        va = torch.full((B,), float("nan"), device="cuda")
+        with torch.no_grad():
+            fused.evaluate_into(x, pr, va)
+        torch.cuda.synchronize()
+        out[flag] = (pr, va)
+    assert torch.equal(out[True][0], out[False][0])
+    assert torch.equal(out[True][1], out[False][1])
+    with torch.no_grad():
+        logits, v = net(x.view(-1, 1, 8, 8))
+    torch.testing.assert_close(out[True][0], torch.softmax(logits, -1), atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(out[True][1], v.reshape(-1), atol=1e-5, rtol=1e-4)
