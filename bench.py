@@ -455,8 +455,13 @@ def cpu_baseline_pool(net_kind, sims, seconds, workers):
     the CPU model and count it was measured on; elsewhere it is reported, not applied."""
     outs = _cpu_pool(net_kind, sims, seconds, workers)
     moves = sum(o["moves"] for o in outs)
-    port = float(sum(o["games_per_s"] for o in outs))  # the measured cores together
-    per_core = port / workers
+    # worker w times the plies from w*60/W on, so a game's length in seconds is 60 x the
+    # MEAN seconds per move over the workers (averaging per-worker game rates instead
+    # would let the cheap end-game moves of the last workers dominate)
+    s_per_move = [o["seconds"] / max(1, o["moves"]) for o in outs]
+    s_per_game = REF_PLIES_PER_GAME * float(np.mean(s_per_move))
+    per_core = 1.0 / s_per_game
+    port = per_core * workers  # the measured cores together
     n_host = os.cpu_count() or workers
     model = cpu_model()
     cal = json.load(open(CALIBRATION_JSON)) if os.path.exists(CALIBRATION_JSON) else None
@@ -478,14 +483,15 @@ def cpu_baseline_pool(net_kind, sims, seconds, workers):
                       f"job) at once; worker w plays from ply w*{int(REF_PLIES_PER_GAME)}/"
                       f"{workers} (seeded random opening) for {seconds:.0f} s of {sims}-sim "
                       f"moves ({moves} moves in all); {net_name} fp32 batch-1 torch-CPU, "
-                      f"oracle/mcts.py SeqMCTS; per worker games/s = 1/(s_per_move x "
-                      f"{REF_PLIES_PER_GAME:.0f} plies); value = mean per-core rate x "
-                      f"os.cpu_count() = {n_host} (independent game processes scale by core; "
-                      "on an SMT host this overstates the CPU)"
+                      f"oracle/mcts.py SeqMCTS; seconds per game = {REF_PLIES_PER_GAME:.0f} x the "
+                      f"mean seconds per move over the workers ({s_per_game:.1f} s); value = "
+                      f"os.cpu_count() = {n_host} cores / seconds per game (independent game "
+                      "processes scale by core; on an SMT host this overstates the CPU)"
                       + (f" x calibration_ratio {ratio:.3f}" if ratio else
                          "; uncalibrated: the calibration's CPU differs, and the port is faster "
                          "than the reference there (ratio < 1), so this overstates the CPU"),
-            "per_worker_games_per_s": [round(o["games_per_s"], 5) for o in outs]}
+            "seconds_per_game": round(s_per_game, 3),
+            "per_worker_s_per_move": [round(t, 4) for t in s_per_move]}
 
 
 STAT_KEYS = ("moves", "games_done", "sims", "plies_total", "games_total", "window_s")
