@@ -91,6 +91,10 @@ SIGNATURES = {
     "az_select": [_P, _P, _P, _P],
     "az_expand_backup": [_P, _P, _P, _P],
     "az_play": [_P, _P],
+    "az_engine_defer_moves": [_P, _I32],
+    "az_select_move": [_P, _P, _P, _I32, _P],
+    "az_expand_backup_par": [_P, _P, _P, _I32, _P],
+    "az_move_flush": [_P, _I32, _P],
     "az_inject": [_P, _P, _P, _P],
     "az_root_policy": [_P, _I32, _D, _D, _P, _P, _P, _P],
     "az_make_move": [_P, _I32, _I32, _P],

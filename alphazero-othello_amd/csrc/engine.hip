@@ -121,6 +121,9 @@ struct Games {
   int32_t* winner;
   int32_t* overflow;
   int32_t* start_step; // slot becomes active at this engine step (stagger)
+  int32_t* sstep;      // deferred moves: the slot's own step count (its k_select calls)
+  int32_t* moving;     // deferred moves: the slot step whose search finished (the next
+                       // step's k_select skips the slot while k_move re-roots it)
   uint32_t* rng_event; // per-slot RNG event counter
   uint8_t* sym;        // [G, K] D4 transform of each pending leaf
   int32_t* noise_cur;  // injected-stream cursors
@@ -143,7 +146,8 @@ struct Counters {  // device-side, 64-bit
   unsigned long long sims;
   unsigned long long moves;
   long long start_budget;  // games still allowed to start (refill)
-  int32_t ready_n;         // slots whose search finished this step (k_move's work list)
+  int32_t ready_n[2];      // k_move's work lists: slots whose search finished in a step of
+                           // parity q (list 0 only, unless moves are deferred)
   int32_t unlimited;       // refill without a start budget
   int32_t move_done;       // k_move workgroups finished this step (the last one resets)
 };
@@ -163,7 +167,7 @@ struct Params {
   Games g;
   Samples s;
   Counters* ctr;
-  int32_t* ready;  // [G]
+  int32_t* ready;  // [2][G] the two work lists
   const double* inj_noise;  // [G, NS, 65]
   const double* inj_u;      // [G, NU]
   int32_t G, C, T, NS, NU;
@@ -171,6 +175,7 @@ struct Params {
   int32_t K;  // leaves per slot per step (virtual loss, MCTS_model.py num_threads)
   int32_t n_explore;
   int32_t eval_mode, rng_mode, d4, auto_play, refill;
+  int32_t defer;   // deferred moves (az_engine_defer_moves)
   double c_puct, alpha, eps, temp, lambd;
   uint64_t seed;
   uint32_t stream_id;
@@ -416,9 +421,11 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
   return r;
 }
 
-__device__ void push_ready(const Params& p, int g) {
-  const int i = atomicAdd(&p.ctr->ready_n, 1);
-  p.ready[i] = g;
+// list q: 0, or with deferred moves the step's parity; sst: the slot's step (deferred)
+__device__ void push_ready(const Params& p, int g, int q = 0, int sst = 0) {
+  const int i = atomicAdd(&p.ctr->ready_n[q], 1);
+  p.ready[q * p.G + i] = g;
+  if (p.defer) p.g.moving[g] = sst;
 }
 
 // ---------------------------------------------------------------------------------
@@ -496,19 +503,46 @@ __device__ NodeRec select_child_vl(const Params& p, int g, int half, const NodeR
 // descents run one after another, each seeing the earlier ones' virtual loss; terminal
 // descents back up at once, the others wait for the batched evaluation in rows
 // nn_in[g*K + j] (the interleaving tests/golden/make_vl_goldens.py forces on the reference).
-template <int KMAX>
+__device__ __forceinline__ void move_body(const Params& p, int q, int deferred, int nblocks,
+                                          int bid);
+
+// par / move_blocks (deferred moves, az_select_move): the first move_blocks workgroups run the
+// move phase of the previous step's list (par ^ 1) while the others descend; a slot whose
+// move is in that list is skipped (nothing of it is read: k_move writes it concurrently, and
+// those writes become visible at the launch boundary) and plays again next step.
+template <int KMAX, bool MERGED = false>
 __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restrict__ nn_in,
                                                       int32_t* __restrict__ leaf_o,
-                                                      int max_descents) {
-  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+                                                      int max_descents, int par,
+                                                      int move_blocks) {
+  if constexpr (MERGED) {  // a separate instantiation: the plain one keeps its registers
+    if ((int)blockIdx.x < move_blocks) {
+      move_body(p, par ^ 1, 1, move_blocks, (int)blockIdx.x);
+      return;
+    }
+  } else {
+    move_blocks = 0;
+  }
+  const int g = ((int)blockIdx.x - move_blocks) * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   const int K = KMAX == 1 ? 1 : p.K;
   const int64_t row0 = (int64_t)g * K;
   const int lane = lane_id();
   // every per-slot word in one round trip
   ENG_STAMP_BEGIN(3);
+  int sst = 0;  // deferred moves: this slot's step (its own count of select calls)
+  if (p.defer) {
+    sst = p.g.sstep[g];
+    if (lane == 0) p.g.sstep[g] = sst + 1;
+    if (p.g.moving[g] == sst - 1) {
+      for (int j = 0; j < K; ++j) emit_none(nn_in, leaf_o, row0 + j);
+      return;
+    }
+  }
   const int status = p.g.status[g];
-  const unsigned long long step = p.ctr->step;
+  // the stagger schedule counts steps: the engine's, or the slot's own with deferred moves
+  // (the engine's counter is advanced inside a deferred launch)
+  const unsigned long long step = p.defer ? (unsigned long long)sst : p.ctr->step;
   const int start_step = p.g.start_step[g];
   const int half = p.g.half[g];
   int sims_done = p.g.sims_done[g];
@@ -603,7 +637,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       p.g.sims_done[g] = sims_done;
     }
     if (w.n == 0 && sims_done >= target) {
-      if (p.auto_play) push_ready(p, g);
+      if (p.auto_play) push_ready(p, g, par, sst);
       else p.g.status[g] = kSearchDone;
     }
     if (deep) {
@@ -827,7 +861,8 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, const Lea
 // of the evaluation batch, the list ends at the first -1).
 template <int KMAX>
 __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
-                                                      const float* __restrict__ values) {
+                                                      const float* __restrict__ values,
+                                                      int par) {
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   const int K = KMAX == 1 ? 1 : p.K;
@@ -886,7 +921,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
       p.g.sims_acc[g] += (unsigned long long)n_sims;
     }
     if (sd >= target) {
-      if (p.auto_play) push_ready(p, g);
+      if (p.auto_play) push_ready(p, g, par, p.defer ? p.g.sstep[g] - 1 : 0);
       else p.g.status[g] = kSearchDone;
     }
   }
@@ -1314,16 +1349,20 @@ __device__ void finish_game(const Params& p, int g, int n_plies, int winner, int
 }
 
 // k_move: one workgroup per slot in the ready list.
-__global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
+// The move phase on work list q by `nblocks` workgroups (this one: bid).  deferred: called
+// from k_select's extra workgroups for the previous step's list, beside that step's
+// descents; the step counter is then advanced but nothing in that launch reads it.
+__device__ __forceinline__ void move_body(const Params& p, int q, int deferred, int nblocks,
+                                          int bid) {
   extern __shared__ __align__(16) int32_t map[];
   __shared__ float s_pi[65];
   __shared__ double s_cdf[65];
   __shared__ int s_child, s_term, s_winner, s_restart;
   const int tid = threadIdx.x;
-  const int n_ready = p.ctr->ready_n;
-  for (int ri = blockIdx.x; ri < n_ready; ri += gridDim.x) {
+  const int n_ready = p.ctr->ready_n[q];
+  for (int ri = bid; ri < n_ready; ri += nblocks) {
     ENG_STAMP_BEGIN(1);
-    const int g = p.ready[ri];
+    const int g = p.ready[q * p.G + ri];
     const int half = p.g.half[g];
     const int ply = p.g.ply[g];
     const int player = p.g.root_player[g];
@@ -1473,13 +1512,18 @@ __global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
   // work list for the next step and advances the step counter: no separate memset launch
   if (tid == 0) {
     __threadfence();
-    if (atomicAdd(&p.ctr->move_done, 1) == (int)gridDim.x - 1) {
-      p.ctr->ready_n = 0;
+    if (atomicAdd(&p.ctr->move_done, 1) == nblocks - 1) {
+      p.ctr->ready_n[q] = 0;
       p.ctr->move_done = 0;
       p.ctr->step += 1;
       __threadfence();
     }
   }
+  (void)deferred;
+}
+
+__global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
+  move_body(p, 0, 0, (int)gridDim.x, (int)blockIdx.x);
 }
 
 // ctr->sims = sum of the slots' counters (one workgroup; az_counters only)
@@ -1515,10 +1559,13 @@ __global__ void k_reset(Params p, long long budget, int stagger) {
     p.ctr->step = 0;
     p.ctr->sims = 0;
     p.ctr->moves = 0;
-    p.ctr->ready_n = 0;
+    p.ctr->ready_n[0] = 0;
+    p.ctr->ready_n[1] = 0;
     p.ctr->move_done = 0;
   }
   if (g >= p.G) return;
+  p.g.sstep[g] = 0;
+  p.g.moving[g] = -2;
   p.g.half[g] = 0;
   p.g.overflow[g] = 0;
   p.g.sims_acc[g] = 0;
@@ -1803,6 +1850,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   p.eval_mode = cfg.eval_mode;
   p.rng_mode = cfg.rng_mode;
   p.d4 = cfg.d4_augment ? 1 : 0;
+  p.defer = 0;
   p.auto_play = cfg.auto_play ? 1 : 0;
   p.refill = cfg.refill ? 1 : 0;
   p.c_puct = cfg.c_puct;
@@ -1846,6 +1894,8 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.g.winner, G));
   chk(dalloc(e, &p.g.overflow, G));
   chk(dalloc(e, &p.g.start_step, G));
+  chk(dalloc(e, &p.g.sstep, G));
+  chk(dalloc(e, &p.g.moving, G));
   chk(dalloc(e, &p.g.rng_event, G));
   chk(dalloc(e, &p.g.sym, GK));
   chk(dalloc(e, &p.g.noise_cur, G));
@@ -1863,7 +1913,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.s.player, (size_t)p.s.cap));
   chk(dalloc(e, &p.s.slot, (size_t)p.s.cap));
   chk(dalloc(e, &p.ctr, 1));
-  chk(dalloc(e, &p.ready, G));
+  chk(dalloc(e, &p.ready, 2 * G));
   double* noise = nullptr;
   double* uni = nullptr;
   if (cfg.rng_mode == AZ_RNG_INJECTED) {
@@ -1893,6 +1943,19 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
       hipFuncSetAttribute((const void*)k_reroot, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_reroot_slots, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      // k_select carries the deferred move phase (az_select_move)
+      hipFuncSetAttribute((const void*)k_select<1, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<2, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<4, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<kMaxLeaves, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess) {
     (void)hipGetLastError();
   }
@@ -1902,13 +1965,14 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   // device allocation would otherwise hold a previous engine's values (out-of-range
   // halves, child ranges).
   bool zero_ok = hipMemset(p.ctr, 0, sizeof(Counters)) == hipSuccess &&
+                 hipMemset(p.g.moving, 0x80, G * sizeof(int32_t)) == hipSuccess &&  // never a step
                  hipMemset(p.g.leaf, 0xff, GK * sizeof(int32_t)) == hipSuccess &&
                  hipMemset(p.g.path_len, 0, GK * sizeof(int32_t)) == hipSuccess &&
                  hipMemset(p.a.flags, 0, nodes) == hipSuccess &&
                  hipMemset(p.a.nchild, 0, nodes) == hipSuccess;
   for (int32_t* a : {p.g.status, p.g.half, p.g.n_nodes, p.g.sims_done, p.g.sims_target,
                      p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
-                     p.g.start_step, p.g.noise_cur, p.g.u_cur})
+                     p.g.start_step, p.g.sstep, p.g.noise_cur, p.g.u_cur})
     zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
   zero_ok = zero_ok && hipMemset(p.g.sims_acc, 0, G * sizeof(unsigned long long)) == hipSuccess &&
             hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
@@ -1969,9 +2033,9 @@ int az_begin_search(az_engine* e, int32_t slot, int32_t num_simulations, void* s
   return AZ_OK;
 }
 
-int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
-  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select: null argument");
-  hipStream_t s = azc::as_stream(stream);
+// k_select (+ the deferred move phase in its first move_blocks workgroups)
+static int launch_select(az_engine* e, float* nn_in, int32_t* leaf_o, int par, int move_blocks,
+                         hipStream_t s) {
   // Simulations that end on a terminal node need no evaluation and run inside the select
   // call; cap them per step so one end-game tree (every simulation terminal) cannot hold
   // the whole batched step for hundreds of dependent descents.  Host-driven engines step
@@ -1984,24 +2048,81 @@ int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
   // leaves, another legal interleaving of the reference's workers)
   const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4 * e->p.K)
                                           : 4 * (e->p.sims + 1) + 64;
+  const dim3 grid(sel_grid(e) + (unsigned)move_blocks);
+  const size_t lds = move_blocks ? e->lds_move : 0;  // the move phase's re-root scratch
   // the kernels' per-leaf arrays sized to the next power of two >= K (registers)
+#define AZ_SEL_GO(KM)                                                                       \
+  do {                                                                                     \
+    if (move_blocks)                                                                       \
+      hipLaunchKernelGGL((k_select<KM, true>), grid, dim3(kSelBlock), lds, s, e->p, nn_in,  \
+                         leaf_o, max_descents, par, move_blocks);                          \
+    else                                                                                   \
+      hipLaunchKernelGGL((k_select<KM, false>), grid, dim3(kSelBlock), lds, s, e->p, nn_in, \
+                         leaf_o, max_descents, par, 0);                                    \
+  } while (0)
   if (e->p.K == 1)
-    hipLaunchKernelGGL(k_select<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
-                       leaf_o, max_descents);
+    AZ_SEL_GO(1);
   else if (e->p.K <= 2)
-    hipLaunchKernelGGL(k_select<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
-                       leaf_o, max_descents);
+    AZ_SEL_GO(2);
   else if (e->p.K <= 4)
-    hipLaunchKernelGGL(k_select<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, nn_in,
-                       leaf_o, max_descents);
+    AZ_SEL_GO(4);
   else
-    hipLaunchKernelGGL(k_select<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
-                       nn_in, leaf_o, max_descents);
+    AZ_SEL_GO(kMaxLeaves);
+#undef AZ_SEL_GO
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
 
-int az_expand_backup(az_engine* e, const float* priors, const float* values, void* stream) {
+static int move_blocks_for(const az_engine* e) { return e->p.G < 64 ? e->p.G : 64; }
+
+int az_select(az_engine* e, float* nn_in, int32_t* leaf_o, void* stream) {
+  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select: null argument");
+  AZ_REQUIRE(!e->p.defer, AZ_ERR_STATE, "az_select: deferred moves are on (az_select_move)");
+  return launch_select(e, nn_in, leaf_o, 0, 0, azc::as_stream(stream));
+}
+
+int az_engine_defer_moves(az_engine* e, int32_t on) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(e->p.auto_play || !on, AZ_ERR_STATE, "deferred moves need an auto-play engine");
+  e->p.defer = on ? 1 : 0;
+  return AZ_OK;
+}
+
+int az_select_move(az_engine* e, float* nn_in, int32_t* leaf_o, int32_t par, void* stream) {
+  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select_move: null argument");
+  AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_select_move: deferred moves are off");
+  AZ_REQUIRE(par == 0 || par == 1, AZ_ERR_ARG, "az_select_move: par must be 0 or 1");
+  return launch_select(e, nn_in, leaf_o, par, move_blocks_for(e), azc::as_stream(stream));
+}
+
+int az_move_flush(az_engine* e, int32_t par, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_move_flush: deferred moves are off");
+  AZ_REQUIRE(par == 0 || par == 1, AZ_ERR_ARG, "az_move_flush: par must be 0 or 1");
+  // the move phase of a step of parity `par` alone: a k_select launch with no slot
+  // workgroups (move list par = (par ^ 1) ^ 1)
+  hipStream_t s = azc::as_stream(stream);
+  const int mb = move_blocks_for(e);
+  const dim3 grid((unsigned)mb);
+  const int q = par ^ 1;
+  if (e->p.K == 1)
+    hipLaunchKernelGGL((k_select<1, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
+                       nullptr, 0, q, mb);
+  else if (e->p.K <= 2)
+    hipLaunchKernelGGL((k_select<2, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
+                       nullptr, 0, q, mb);
+  else if (e->p.K <= 4)
+    hipLaunchKernelGGL((k_select<4, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
+                       nullptr, 0, q, mb);
+  else
+    hipLaunchKernelGGL((k_select<kMaxLeaves, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p,
+                       nullptr, nullptr, 0, q, mb);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+static int launch_expand(az_engine* e, const float* priors, const float* values, int par,
+                         void* stream) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
              "az_expand_backup: priors/values required in external-eval mode");
@@ -2012,22 +2133,37 @@ int az_expand_backup(az_engine* e, const float* priors, const float* values, voi
   }
   if (e->p.K == 1)
     hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
-                       values);
+                       values, par);
   else if (e->p.K <= 2)
     hipLaunchKernelGGL(k_expand<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
-                       values);
+                       values, par);
   else if (e->p.K <= 4)
     hipLaunchKernelGGL(k_expand<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
-                       values);
+                       values, par);
   else
     hipLaunchKernelGGL(k_expand<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
-                       priors, values);
+                       priors, values, par);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
 
+int az_expand_backup(az_engine* e, const float* priors, const float* values, void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(!e->p.defer, AZ_ERR_STATE, "az_expand_backup: deferred moves are on (use _par)");
+  return launch_expand(e, priors, values, 0, stream);
+}
+
+int az_expand_backup_par(az_engine* e, const float* priors, const float* values, int32_t par,
+                         void* stream) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_expand_backup_par: deferred moves are off");
+  AZ_REQUIRE(par == 0 || par == 1, AZ_ERR_ARG, "az_expand_backup_par: par must be 0 or 1");
+  return launch_expand(e, priors, values, par, stream);
+}
+
 int az_play(az_engine* e, void* stream) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  AZ_REQUIRE(!e->p.defer, AZ_ERR_STATE, "az_play: deferred moves are on (az_select_move)");
   hipStream_t s = azc::as_stream(stream);
   if (!e->p.auto_play) {
     hipLaunchKernelGGL(k_tick, dim3(1), dim3(1), 0, s, e->p.ctr);

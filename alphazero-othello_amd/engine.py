@@ -109,6 +109,23 @@ class Engine:
     def play(self):
         nat.check(nat.lib.az_play(self.h, self._s()), "az_play")
 
+    # deferred moves (include/az_othello.h): step n's move phase inside step n+1's select launch
+    def defer_moves(self, on=True):
+        nat.check(nat.lib.az_engine_defer_moves(self.h, int(bool(on))), "az_engine_defer_moves")
+
+    def select_move(self, par):
+        nat.check(nat.lib.az_select_move(self.h, nat.ptr(self.nn_in), nat.ptr(self.leaf), int(par),
+                                         self._s()), "az_select_move")
+
+    def expand_par(self, par, priors=None, values=None):
+        pr = self.priors if priors is None else priors
+        va = self.values if values is None else values
+        nat.check(nat.lib.az_expand_backup_par(self.h, nat.ptr(pr), nat.ptr(va), int(par),
+                                               self._s()), "az_expand_backup_par")
+
+    def move_flush(self, par):
+        nat.check(nat.lib.az_move_flush(self.h, int(par), self._s()), "az_move_flush")
+
     # ---- synchronous control --------------------------------------------------------
     def reset_all(self, start_budget=-1, stagger_steps=0):
         nat.check(nat.lib.az_reset_all(self.h, int(start_budget), int(stagger_steps), self._s()),
@@ -260,7 +277,7 @@ class BatchedSelfPlay:
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
                  device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1,
-                 require_graph=False):
+                 require_graph=False, defer_moves=True):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -281,6 +298,13 @@ class BatchedSelfPlay:
             self.net = inference_copy(net, self.device, dtype, precision=precision)
         else:
             self.net = net.to(self.device).eval()
+        # defer_moves: each step's move phase (pi, sample, record, re-root) runs in the next
+        # step's select launch beside its descents instead of after expand (per game nothing
+        # changes); steps alternate a parity the graphs are captured with
+        self.defer_moves = bool(defer_moves)
+        if self.defer_moves:
+            self.engine.defer_moves(True)
+        self._par = 0  # parity of the next step (deferred moves)
         self.use_graph = use_graph
         # require_graph: a failed capture raises instead of running eagerly (bench.py: a
         # regression must not show up only as lost throughput)
@@ -289,9 +313,12 @@ class BatchedSelfPlay:
         self.steps_per_graph = max(1, int(steps_per_graph))
         self.graph = None  # {steps: CUDAGraph}: one replay = that many simulation steps
 
-    def _step_body(self):
+    def _step_body(self, par=0):
         e = self.engine
-        e.select()
+        if self.defer_moves:
+            e.select_move(par)  # + the previous step's moves
+        else:
+            e.select()
         if self.net is not None:
             if hasattr(self.net, "evaluate_into"):
                 self.net.evaluate_into(e.nn_in, e.priors, e.values)
@@ -299,8 +326,11 @@ class BatchedSelfPlay:
                 pr, va = self.net.evaluate_planes(e.nn_in)
                 e.priors.copy_(pr)
                 e.values.copy_(va)
-        e.expand()
-        e.play()
+        if self.defer_moves:
+            e.expand_par(par)
+        else:
+            e.expand()
+            e.play()
 
     def _capture(self):
         """Capture the step into HIP graphs: one of `steps_per_graph` consecutive steps (the
@@ -311,15 +341,23 @@ class BatchedSelfPlay:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm MIOpen / hipBLASLt solution caches outside capture
-                self._step_body()
+                self._step_body(self._par)
+                self._par ^= 1
         torch.cuda.current_stream().wait_stream(s)
+        # graphs keyed by (steps, parity of their first step): the multi-step graph starts at
+        # parity 0 (an even number of steps keeps it there), one single step per parity
+        k = self.steps_per_graph + (self.steps_per_graph & 1 if self.defer_moves else 0)
+        self.steps_per_graph = k
         graphs = {}
-        for k in sorted({1, self.steps_per_graph}):
+        for key in [(k, 0), (1, 0), (1, 1)] if self.defer_moves else [(k, 0), (1, 0)]:
+            if key in graphs:
+                continue
+            n, par = key
             g = torch.cuda.CUDAGraph()  # private memory pool per graph
             with torch.no_grad(), torch.cuda.graph(g):
-                for _ in range(k):
-                    self._step_body()
-            graphs[k] = g
+                for i in range(n):
+                    self._step_body(par ^ (i & 1))
+            graphs[key] = g
         self.graph = graphs
 
     def reset(self, start_budget=-1, stagger_steps=0):
@@ -340,13 +378,24 @@ class BatchedSelfPlay:
                 warnings.warn(f"HIP graph capture failed, running the step eagerly: {ex!r}")
         if self.graph is None:
             for _ in range(n):
-                self._step_body()
-            return
-        k = self.steps_per_graph
-        for _ in range(n // k):
-            self.graph[k].replay()
-        for _ in range(n % k):
-            self.graph[1].replay()
+                self._step_body(self._par)
+                if self.defer_moves:
+                    self._par ^= 1
+        else:
+            k = self.steps_per_graph
+            left = n
+            while left > 0:
+                if left >= k and self._par == 0:
+                    self.graph[(k, 0)].replay()  # k even with deferred moves: parity kept
+                    left -= k
+                else:
+                    self.graph[(1, self._par)].replay()
+                    left -= 1
+                    if self.defer_moves:
+                        self._par ^= 1
+        if self.defer_moves and n > 0:
+            # the last step's moves, so results read after step() returns are complete
+            self.engine.move_flush(self._par ^ 1)
 
     def play_games(self, n_games, max_steps=None, check_every=256):
         """Play exactly n_games complete games (slots restart until the budget is used);

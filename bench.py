@@ -105,6 +105,9 @@ def parse():
                          "products, fp32-accurate; fp32 = fp32 MFMA; fp16 = fp16 operands "
                          "(c5's fp16 inference)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="the move phase after expand (az_play) instead of inside the next "
+                         "step's select launch (deferred moves, the default)")
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="simulation steps captured per HIP graph (rocprofv3's kernel tracer "
                          "records 8-step graphs completely: DESIGN.md section 5)")
@@ -562,6 +565,7 @@ def main():
                          device=device, d4_augment=a.d4,
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
                          sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
+                         defer_moves=not a.no_defer,
                          precision=a.conv_precision, leaves_per_step=a.leaves)
     e = sp.engine
     if os.environ.get("AZ_DUMP_MAPS"):  # diagnostics: the address map, to place a fault's PC
@@ -639,7 +643,8 @@ def main():
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
                    "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
-                   "hip_graph": sp.graph is not None, "graph_error": sp.graph_error},
+                   "hip_graph": sp.graph is not None, "graph_error": sp.graph_error,
+                   "deferred_moves": sp.defer_moves},
         "value_basis": basis,
         "detail": {"moves": int(moves_all),
                    "moves_based_games_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),

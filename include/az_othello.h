@@ -191,6 +191,21 @@ int az_expand_backup(az_engine* eng, const float* priors, const float* values, v
 /* auto-play move phase (see above); host-driven engines: step counter only. */
 int az_play(az_engine* eng, void* stream);
 
+/* Deferred moves (auto-play engines, reference self_play_worker.py:69-86 per game unchanged):
+ * after az_engine_defer_moves(eng, 1) a step is az_select_move -> evaluation ->
+ * az_expand_backup_par with the step's parity par (0, 1, 0, 1, ...), and there is no
+ * az_play: the move phase of step n runs inside step n+1's az_select_move launch, in extra
+ * workgroups beside the descents (which skip the slots being moved; they play again the step
+ * after), so the two latency-bound phases overlap in one launch.  Each slot's games, samples
+ * and random draws are those of the plain order; only the step a move lands in shifts.
+ * az_move_flush(eng, par) applies the moves of the last step (parity par) before results are
+ * read.  az_select / az_expand_backup / az_play refuse while deferral is on. */
+int az_engine_defer_moves(az_engine* eng, int32_t on);
+int az_select_move(az_engine* eng, float* nn_in, int32_t* leaf_o, int32_t par, void* stream);
+int az_expand_backup_par(az_engine* eng, const float* priors, const float* values, int32_t par,
+                         void* stream);
+int az_move_flush(az_engine* eng, int32_t par, void* stream);
+
 /* AZ_RNG_INJECTED: per-slot streams, noise double [G, inj_noise_slots, 65] (Dirichlet
  * vectors, consumed at each root expansion with epsilon > 0) and uniforms double
  * [G, inj_uniform_slots] (consumed by the temperature-0 tie break and the action sample,
