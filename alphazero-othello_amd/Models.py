@@ -489,6 +489,9 @@ class FusedInferenceNet(nn.Module, Inference):
         kept, least recently used dropped first (a caller evaluating many ragged batch sizes
         does not accumulate buffers).  release_scratch() drops the unpinned ones."""
         sc = self.__dict__.setdefault("_trunk_scratch", {})
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:  # "cuda" and "cuda:0": one entry
+            device = torch.device("cuda", torch.cuda.current_device())
         key = (device, B)
         ent = sc.pop(key, None)  # re-inserted below: dict order = recency
         if ent is None:
@@ -512,13 +515,44 @@ class FusedInferenceNet(nn.Module, Inference):
     # the trunk output's HBM round trip fewer per evaluation).  AZ_FUSE_HEADS=0 turns it off.
     fuse_heads = os.environ.get("AZ_FUSE_HEADS", "1") != "0"
 
-    def _trunk(self, x, heads_into=None):
+    def _stem_stored(self):
+        """Whether the trunk starts with a stored HIP stem output feeding the fp16x2 block
+        convs (the branch of _trunk an engine-side stem can replace)."""
+        c1s, c2s = list(self.c1), list(self.c2)
+        return (isinstance(self.stem, _HipStem) and bool(c1s) and not self._trunk_kernel_ready()
+                and not (self.fuse_stem and getattr(c1s[0], "precision", "fp32") != "fp32"
+                         and c1s[0].algo == "direct" and c2s[0].algo == "direct")
+                and getattr(c1s[0], "precision", "") == "fp16x2")
+
+    def engine_stem(self, device, B):
+        """The stem for the engine that packs the planes to run (az_engine_set_stem): its
+        weights and this batch size's first-activation buffers (NHWC [B, C, 8, 8] and the
+        per-board ranges the first conv reads), pinned for the net's lifetime; None where the
+        trunk does not start from a stored HIP stem on the fp16x2 path.  Calls of
+        evaluate_into(..., stem_done=True) at that batch size then start at the first block."""
+        if not (self._fused_heads_ready() and self._stem_stored()):
+            return None
+        ent = self._scratch(device, B)
+        ent["pinned"] = True
+        C = self.stem.channels
+        if "h0" not in ent:
+            ent["h0"] = torch.empty((B, C, 8, 8), dtype=torch.float32, device=device,
+                                    memory_format=torch.channels_last)
+        return {"w9": self.stem.w9, "bias": self.stem.bias, "y": ent["h0"],
+                "absmax": ent["absmax"][0], "channels": C}
+
+    def _trunk(self, x, heads_into=None, stem_done=False):
         """The trunk's output (NHWC [B, C, 8, 8]); with heads_into = (priors, values) the
         heads may be fused into the last conv, which then writes them and None is returned
-        (evaluate_into falls back to the separate heads kernel on a tensor)."""
+        (evaluate_into falls back to the separate heads kernel on a tensor).  stem_done: the
+        stem's output and ranges are already in this batch size's engine_stem buffers."""
         if x.dim() == 3:
             x = x.unsqueeze(1)
         x = x.contiguous(memory_format=torch.channels_last)
+        if stem_done:
+            ent = self._scratch(x.device, x.shape[0])
+            if not (self._stem_stored() and "h0" in ent):
+                raise RuntimeError("stem_done without engine_stem buffers for this batch size")
         if self._trunk_kernel_ready():
             import az_native as nat
 
@@ -547,7 +581,9 @@ class FusedInferenceNet(nn.Module, Inference):
             B = x.shape[0]
             ent = self._scratch(x.device, B)
             bufs = ent["absmax"]
-            if isinstance(self.stem, _HipStem):
+            if stem_done:  # written by the engine's select launch (engine_stem)
+                h = ent["h0"]
+            elif isinstance(self.stem, _HipStem):
                 h = self.stem(x, absmax=bufs[0])
             else:
                 h = self.stem(x)
@@ -595,10 +631,13 @@ class FusedInferenceNet(nn.Module, Inference):
             }
         return True
 
-    def evaluate_into(self, planes, priors, values):
+    def evaluate_into(self, planes, priors, values, stem_done=False):
         """Leaf evaluation straight into the engine's buffers: priors float32 [B, 65]
         (softmax), values float32 [B] (tanh).  AlphaZeroNet on the HIP trunk runs both heads
-        in one kernel (csrc/heads.hip); otherwise the module's heads + copies."""
+        in one kernel (csrc/heads.hip); otherwise the module's heads + copies.  stem_done:
+        the engine has run the stem into engine_stem's buffers (planes are then not read)."""
+        if stem_done and not self._fused_heads_ready():
+            raise RuntimeError("stem_done on a net without an engine stem")
         if not self._fused_heads_ready():
             p, v = self.evaluate_planes(planes)
             priors.copy_(p)
@@ -607,7 +646,8 @@ class FusedInferenceNet(nn.Module, Inference):
         import az_native as nat
 
         B = planes.shape[0]
-        h = self._trunk(planes.view(B, 1, 8, 8), heads_into=(priors, values))
+        h = self._trunk(planes.view(B, 1, 8, 8), heads_into=(priors, values),
+                        stem_done=stem_done)
         if h is None:  # the heads ran in the last conv's epilogue
             return
         hw = self._hw

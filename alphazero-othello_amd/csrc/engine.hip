@@ -29,6 +29,7 @@
 
 #include <cstdlib>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "bitboard.h"
@@ -176,6 +177,12 @@ struct Params {
   int32_t n_explore;
   int32_t eval_mode, rng_mode, d4, auto_play, refill;
   int32_t defer;   // deferred moves (az_engine_defer_moves)
+  // the evaluation's stem computed by the wave that packs each row (az_engine_set_stem)
+  const float* stem_w;  // [9][stem_c] tap-major
+  const float* stem_b;  // [stem_c]
+  float* stem_y;        // [G*K][64][stem_c] NHWC fp32
+  float* stem_amax;     // [G*K] each row's max |y| (optional)
+  int32_t stem_c;       // 0 (off), 64 or 128
   double c_puct, alpha, eps, temp, lambd;
   uint64_t seed;
   uint32_t stream_id;
@@ -300,19 +307,110 @@ __device__ void backup_path(const Params& p, int g, int half, int path_node, int
   }
 }
 
-// Pack the canonical NN input player*state (Models.py:16): own stones +1, opponent -1,
-// optionally through D4 transform `sym` (random_symmetry, MCTS_model.py:15-28).
-__device__ void emit_leaf(const Params& p, float* nn_in, int64_t row, uint64_t own, uint64_t opp,
-                          int sym) {
+// The net's stem (Models.py:179-180, :209: 3x3 conv 1 -> C, BatchNorm folded, ReLU) on the
+// plane row the wave has just packed, when the net hands its stem to the engine
+// (az_engine_set_stem): y[row] NHWC fp32 and the row's max |y| (the fp16x2 trunk's input
+// range).  k_conv_stem's (conv.hip) fmaf chain in its tap order, so bit-identical to it.
+// pl = the plane's value at square `lane`; lane = channels V*lane .. V*lane + V - 1.
+#ifndef AZ_STEM_NOSTORE
+#define AZ_STEM_NOSTORE 0
+#endif
+#ifndef AZ_STEM_CODE
+#define AZ_STEM_CODE 1  // experiment builds: 0 compiles the engine stem out
+#endif
+// One board row py of the stem: tap rows dy in [DYLO, DYHI] exist (compile time, as the
+// columns: no branch per tap), so the top and bottom rows are separate code and the six
+// inner rows one loop.
+template <int C, int DYLO, int DYHI, class VecT>
+__device__ __forceinline__ void stem_board_row(const VecT (&w)[9], VecT b, float pl, int py,
+                                               VecT* __restrict__ y, float& bmax) {
+  constexpr int V = C / kWave;
+  float v[3][8];  // the plane's rows py-1 .. py+1 (uniform)
+#pragma unroll
+  for (int dy = DYLO; dy <= DYHI; ++dy)
+#pragma unroll
+    for (int x = 0; x < 8; ++x) v[dy + 1][x] = readlane(pl, (py + dy) * 8 + x);
+#pragma unroll
+  for (int px = 0; px < 8; ++px) {
+    VecT acc = b;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, xx = px + t % 3 - 1;
+      if (dy < DYLO || dy > DYHI || xx < 0 || xx > 7) continue;
+      if constexpr (V == 2) {
+        acc.x = fmaf(v[dy + 1][xx], w[t].x, acc.x);
+        acc.y = fmaf(v[dy + 1][xx], w[t].y, acc.y);
+      } else {
+        acc = fmaf(v[dy + 1][xx], w[t], acc);
+      }
+    }
+    if constexpr (V == 2) {
+      acc.x = fmaxf(acc.x, 0.f);
+      acc.y = fmaxf(acc.y, 0.f);
+      bmax = fmaxf(bmax, fmaxf(acc.x, acc.y));
+    } else {
+      acc = fmaxf(acc, 0.f);
+      bmax = fmaxf(bmax, acc);
+    }
+#if !AZ_STEM_NOSTORE  // experiment builds: the stem's arithmetic without its stores
+    y[(py * 8 + px) * (C / V)] = acc;
+#endif
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void stem_row(const Params& p, int64_t row, float pl) {
+  constexpr int V = C / kWave;
+  using VecT = typename std::conditional<V == 2, float2, float>::type;
   const int lane = lane_id();
-  const float v = ((own >> lane) & 1) ? 1.0f : (((opp >> lane) & 1) ? -1.0f : 0.0f);
-  const int dst = sym ? azb::d4_square(lane, sym) : lane;
-  nn_in[row * 64 + dst] = v;
+  VecT w[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) w[t] = reinterpret_cast<const VecT*>(p.stem_w + t * C)[lane];
+  const VecT b = reinterpret_cast<const VecT*>(p.stem_b)[lane];
+  VecT* y = reinterpret_cast<VecT*>(p.stem_y + row * 64 * C) + lane;
+  float bmax = 0.0f;
+  stem_board_row<C, 0, 1>(w, b, pl, 0, y, bmax);
+#pragma unroll 1
+  for (int py = 1; py < 7; ++py) stem_board_row<C, -1, 1>(w, b, pl, py, y, bmax);
+  stem_board_row<C, -1, 0>(w, b, pl, 7, y, bmax);
+  if (p.stem_amax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, kWave));
+    if (lane == 0) p.stem_amax[row] = bmax;
+  }
+}
+
+__device__ __forceinline__ void emit_stem(const Params& p, int64_t row, float pl) {
+#if !AZ_STEM_CODE
+  return;
+#endif
+  if (p.stem_c == 128) stem_row<128>(p, row, pl);
+  else if (p.stem_c == 64) stem_row<64>(p, row, pl);
+}
+
+// Pack the canonical NN input player*state (Models.py:16): own stones +1, opponent -1,
+// optionally through D4 transform `sym` (random_symmetry, MCTS_model.py:15-28; square q of
+// the transformed board is bit q of d4(own) / d4(opp)).
+// Returns the value stored (the stem's input at square `lane`).
+__device__ float emit_leaf(float* nn_in, int64_t row, uint64_t own, uint64_t opp, int sym) {
+  const int lane = lane_id();
+  const uint64_t P = sym ? azb::d4(own, sym) : own, N = sym ? azb::d4(opp, sym) : opp;
+  const float pl = ((P >> lane) & 1) ? 1.0f : (((N >> lane) & 1) ? -1.0f : 0.0f);
+  nn_in[row * 64 + lane] = pl;
+  return pl;
 }
 
 __device__ void emit_none(float* nn_in, int32_t* leaf_o, int64_t row) {
   nn_in[row * 64 + lane_id()] = 0.0f;
   if (lane_id() == 0 && leaf_o) leaf_o[row] = -1;
+}
+
+// rows without a leaf (skipped / idle slots): the stem of an empty board
+__device__ void emit_none_rows(const Params& p, float* nn_in, int32_t* leaf_o, int64_t row0,
+                               int K) {
+  for (int j = 0; j < K; ++j) emit_none(nn_in, leaf_o, row0 + j);
+  if (p.stem_c)
+    for (int j = 0; j < K; ++j) emit_stem(p, row0 + j, 0.0f);
 }
 
 // What the descent needs of a node, loaded together with its siblings' PUCT inputs so that
@@ -535,7 +633,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
     sst = p.g.sstep[g];
     if (lane == 0) p.g.sstep[g] = sst + 1;
     if (p.g.moving[g] == sst - 1) {
-      for (int j = 0; j < K; ++j) emit_none(nn_in, leaf_o, row0 + j);
+      emit_none_rows(p, nn_in, leaf_o, row0, K);
       return;
     }
   }
@@ -548,13 +646,17 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   int sims_done = p.g.sims_done[g];
   const int target = p.g.sims_target[g];
   if (status != kActive || (long long)step < (long long)start_step) {
-    for (int j = 0; j < K; ++j) emit_none(nn_in, leaf_o, row0 + j);
+    emit_none_rows(p, nn_in, leaf_o, row0, K);
     return;
   }
   Waiting<KMAX> w;
   w.n = 0;
+  float plane[KMAX];  // the packed rows' values at square `lane` (the stem's inputs)
 #pragma unroll
-  for (int j = 0; j < KMAX; ++j) w.path[j] = -1;
+  for (int j = 0; j < KMAX; ++j) {
+    w.path[j] = -1;
+    plane[j] = 0.0f;
+  }
   bool deep = false;  // a waiting path past kMaxPath: its virtual loss could not be tracked
   int depth = 0;      // depth of the current node
   int path_node = 0;  // lane d: node at depth d of the current descent
@@ -573,7 +675,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
         p.g.sym[row] = (uint8_t)sym;
       }
     }
-    emit_leaf(p, nn_in, row, cur.own, cur.opp, sym);
+    const float pl = emit_leaf(nn_in, row, cur.own, cur.opp, sym);
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj)
+      if (jj == j) plane[jj] = pl;
     const bool held = depth < kMaxPath && lane <= depth;
     if (held) p.g.path[row * kMaxPath + lane] = path_node;
     if (lane == 0) {
@@ -629,6 +734,11 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   for (int j = w.n; j < K; ++j) {
     emit_none(nn_in, leaf_o, row0 + j);
     if (KMAX > 1 && lane == 0) p.g.leaf[row0 + j] = -1;
+  }
+  if (p.stem_c) {
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+      if (j < K) emit_stem(p, row0 + j, plane[j]);
   }
   if (lane == 0) {
     const int prev = p.g.sims_done[g];
@@ -2085,6 +2195,28 @@ int az_engine_defer_moves(az_engine* e, int32_t on) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   AZ_REQUIRE(e->p.auto_play || !on, AZ_ERR_STATE, "deferred moves need an auto-play engine");
   e->p.defer = on ? 1 : 0;
+  return AZ_OK;
+}
+
+int az_engine_set_stem(az_engine* e, const float* w9, const float* bias, float* y,
+                       float* absmax, int32_t channels) {
+  AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
+  if (channels == 0) {
+    e->p.stem_c = 0;
+    e->p.stem_w = e->p.stem_b = nullptr;
+    e->p.stem_y = e->p.stem_amax = nullptr;
+    return AZ_OK;
+  }
+  AZ_REQUIRE(channels == 64 || channels == 128, AZ_ERR_ARG,
+             "az_engine_set_stem: channels must be 0, 64 or 128, got %d", channels);
+  AZ_REQUIRE(w9 && bias && y, AZ_ERR_ARG, "az_engine_set_stem: null buffer");
+  AZ_REQUIRE(((uintptr_t)w9 | (uintptr_t)bias | (uintptr_t)y) % 8 == 0, AZ_ERR_ARG,
+             "az_engine_set_stem: buffers must be 8-byte aligned");
+  e->p.stem_w = w9;
+  e->p.stem_b = bias;
+  e->p.stem_y = y;
+  e->p.stem_amax = absmax;
+  e->p.stem_c = channels;
   return AZ_OK;
 }
 

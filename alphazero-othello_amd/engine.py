@@ -16,6 +16,7 @@ The host only reads counters.  Finished games' samples accumulate in a device bu
 the reference's training-tuple layout (canonical state, pi, target).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -125,6 +126,25 @@ class Engine:
 
     def move_flush(self, par):
         nat.check(nat.lib.az_move_flush(self.h, int(par), self._s()), "az_move_flush")
+
+    def set_stem(self, w9, bias, y, absmax=None):
+        """Run the net's stem inside the select launch (az_engine_set_stem): y float32 NHWC
+        [G*K, C, 8, 8] receives relu(conv3x3(nn_in row) + bias) of every packed row, absmax
+        float32 [G*K] each row's max |y|.  The tensors are kept referenced here.  None turns it
+        off."""
+        if w9 is None:
+            self._stem = None
+            nat.check(nat.lib.az_engine_set_stem(self.h, None, None, None, None, 0),
+                      "az_engine_set_stem")
+            return
+        R = self.G * self.K
+        C = bias.numel()
+        assert w9.dtype == bias.dtype == y.dtype == torch.float32 and w9.shape == (9, C)
+        assert y.numel() == R * 64 * C and y.is_contiguous(memory_format=torch.channels_last)
+        assert absmax is None or (absmax.dtype == torch.float32 and absmax.numel() == R)
+        self._stem = (w9, bias, y, absmax)
+        nat.check(nat.lib.az_engine_set_stem(self.h, nat.ptr(w9), nat.ptr(bias), nat.ptr(y),
+                                             nat.ptr(absmax), C), "az_engine_set_stem")
 
     # ---- synchronous control --------------------------------------------------------
     def reset_all(self, start_budget=-1, stagger_steps=0):
@@ -277,7 +297,7 @@ class BatchedSelfPlay:
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
                  device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1,
-                 require_graph=False, defer_moves=True):
+                 require_graph=False, defer_moves=True, engine_stem=None):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -305,6 +325,17 @@ class BatchedSelfPlay:
         if self.defer_moves:
             self.engine.defer_moves(True)
         self._par = 0  # parity of the next step (deferred moves)
+        # engine_stem: the net's stem runs in the select launch, by the wave that packs each
+        # row (bit-identical; one launch and the planes' round trip fewer per step); default
+        # on where the net supports it, AZ_ENGINE_STEM=0 turns it off
+        if engine_stem is None:
+            engine_stem = os.environ.get("AZ_ENGINE_STEM", "1") != "0"
+        self.engine_stem = False
+        if engine_stem and self.net is not None and hasattr(self.net, "engine_stem"):
+            st = self.net.engine_stem(self.device, self.engine.G * self.engine.K)
+            if st is not None:
+                self.engine.set_stem(st["w9"], st["bias"], st["y"], st["absmax"])
+                self.engine_stem = True
         self.use_graph = use_graph
         # require_graph: a failed capture raises instead of running eagerly (bench.py: a
         # regression must not show up only as lost throughput)
@@ -320,7 +351,9 @@ class BatchedSelfPlay:
         else:
             e.select()
         if self.net is not None:
-            if hasattr(self.net, "evaluate_into"):
+            if self.engine_stem:
+                self.net.evaluate_into(e.nn_in, e.priors, e.values, stem_done=True)
+            elif hasattr(self.net, "evaluate_into"):
                 self.net.evaluate_into(e.nn_in, e.priors, e.values)
             else:
                 pr, va = self.net.evaluate_planes(e.nn_in)

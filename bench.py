@@ -108,6 +108,10 @@ def parse():
     ap.add_argument("--no-defer", action="store_true",
                     help="the move phase after expand (az_play) instead of inside the next "
                          "step's select launch (deferred moves, the default)")
+    ap.add_argument("--no-engine-stem", action="store_true",
+                    help="the net's stem as its own kernel on the packed planes instead of "
+                         "inside the select launch (az_engine_set_stem, the default where the "
+                         "net has a stored fp16x2 stem)")
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="simulation steps captured per HIP graph (rocprofv3's kernel tracer "
                          "records 8-step graphs completely: DESIGN.md section 5)")
@@ -566,6 +570,7 @@ def main():
                          dtype=torch.float16 if a.precision == "fp16" else torch.float32,
                          sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
                          defer_moves=not a.no_defer,
+                         engine_stem=not a.no_engine_stem,
                          precision=a.conv_precision, leaves_per_step=a.leaves)
     e = sp.engine
     if os.environ.get("AZ_DUMP_MAPS"):  # diagnostics: the address map, to place a fault's PC
@@ -644,7 +649,7 @@ def main():
                    "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
                    "hip_graph": sp.graph is not None, "graph_error": sp.graph_error,
-                   "deferred_moves": sp.defer_moves},
+                   "deferred_moves": sp.defer_moves, "engine_stem": sp.engine_stem},
         "value_basis": basis,
         "detail": {"moves": int(moves_all),
                    "moves_based_games_per_s": round(float(moves_all / plies_per_game / t_max), 4), "games_finished_in_window": int(games_all),

@@ -201,6 +201,16 @@ int az_play(az_engine* eng, void* stream);
  * az_move_flush(eng, par) applies the moves of the last step (parity par) before results are
  * read.  az_select / az_expand_backup / az_play refuse while deferral is on. */
 int az_engine_defer_moves(az_engine* eng, int32_t on);
+
+/* The evaluation's stem inside the select launch (replaces the net's first layer,
+ * reference Models.py:179-180, :209, conv0 + bn0 + relu, BatchNorm folded): every row
+ * az_select / az_select_move packs is also run through relu(conv3x3_{1->C}(row) + bias)
+ * by the wave that packed it, into y (float [G*K][64][C], NHWC) and, if absmax is given,
+ * its max |y| into absmax[row] -- bit-identical to az_conv_stem2_gpu on nn_in.
+ * w9: float [9][C] tap-major, bias: float [C]; channels 64 or 128, 0 turns it off.  The
+ * buffers must stay allocated while it is on. */
+int az_engine_set_stem(az_engine* eng, const float* w9, const float* bias, float* y,
+                       float* absmax, int32_t channels);
 int az_select_move(az_engine* eng, float* nn_in, int32_t* leaf_o, int32_t par, void* stream);
 int az_expand_backup_par(az_engine* eng, const float* priors, const float* values, int32_t par,
                          void* stream);
