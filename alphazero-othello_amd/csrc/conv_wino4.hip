@@ -66,7 +66,8 @@
 #endif
 // experiment hooks (scripts/build_variants.py builds with bits set; results wrong):
 // 1 = no weight loads in the loop, 2 = no transform / input work in the loop, 4 = no MFMAs,
-// 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads.  Product: 0.
+// 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads, 32 = weight loads by the
+// first row tile's waves only (the other half reuses stale fragments).  Product: 0.
 #ifndef AZ_W4_EXP
 #define AZ_W4_EXP 0
 #endif
@@ -81,6 +82,11 @@
 // timing proxy of a two-plane split (wrong numerics): 2 planes, 3 products
 #ifndef AZ_W4_PROXY2
 #define AZ_W4_PROXY2 0
+#endif
+// packed / mixed-precision forms of the transform's and fold's float ops (inline asm where
+// the compiler would split them); 0 = the plain vector expressions (A/B builds)
+#ifndef AZ_W4_PK
+#define AZ_W4_PK 1
 #endif
 
 namespace {
@@ -255,9 +261,27 @@ __device__ __forceinline__ void read_a(Frag<G> (&a)[G::NRT], const char* buf, in
       a[t].v[pl] = *reinterpret_cast<const Word8<G>*>(buf + (l * G::PLANES + pl) * G::SLAB + aoff[t]);
 }
 
-template <class G>
+// FIRST: the group's first product on this accumulator takes C = 0 (an inline constant)
+// instead of a zeroed register set, so no per-group zeroing pass is needed
+template <class G, bool FIRST = false>
 __device__ __forceinline__ void mma(f32x16& acc, const Frag<G>& a, const Frag<G>& b) {
-  if constexpr (G::MODE == AZ_CONV_SPLIT3) {
+  if constexpr (FIRST && G::MODE == AZ_CONV_FP16X2) {
+    const f32x16 z = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[1], b.v[0], z, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[0], acc, 0, 0, 0);
+  } else if constexpr (FIRST && G::MODE == AZ_CONV_FP16) {
+    const f32x16 z = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[0], b.v[0], z, 0, 0, 0);
+  } else if constexpr (FIRST) {
+    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+    constexpr int T0 = AZ_W4_PROXY2 ? 3 : 0;
+    const f32x16 z = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[PA[T0]], b.v[PB[T0]], z, 0, 0, 0);
+#pragma unroll
+    for (int t = T0 + 1; t < 6; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[PA[t]], b.v[PB[t]], acc, 0, 0, 0);
+  } else if constexpr (G::MODE == AZ_CONV_SPLIT3) {
     // smallest partial products first (x2y0, x1y1, x0y2, x1y0, x0y1, x0y0)
     constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
     constexpr int T0 = AZ_W4_PROXY2 ? 3 : 0;  // proxy: the last three products only
@@ -372,13 +396,26 @@ __device__ __forceinline__ void combine_k(f32x2 (&rk)[4], const f32x2 (&d)[8], f
   for (int b = 0; b < 4; ++b) rk[b] = __builtin_elementwise_fma(fb, d[4 + b], fa * d[b]);
 }
 
+// a - b on an f32x2 as ONE v_pk_add_f32 with b negated: the compiler splits a two-wide
+// fsub into two v_sub_f32 (and folds an fma by -1 back into that fsub); same IEEE
+// differences element by element
+__device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
+#if AZ_W4_PK
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return a - b;
+#endif
+}
+
 // V at point (k, l) = (row k of B^T d) B: column combination l
 template <int l>
 __device__ __forceinline__ f32x2 col_comb(const f32x2 (&rk)[4]) {
-  if constexpr (l == 0) return rk[0] - rk[2];
+  if constexpr (l == 0) return pk_sub(rk[0], rk[2]);
   if constexpr (l == 1) return rk[1] + rk[2];
-  if constexpr (l == 2) return rk[2] - rk[1];
-  return rk[1] - rk[3];
+  if constexpr (l == 2) return pk_sub(rk[2], rk[1]);
+  return pk_sub(rk[1], rk[3]);
 }
 
 // split two transformed values into PLANES 16-bit words and store them in their slabs
@@ -387,9 +424,22 @@ __device__ __forceinline__ void put(char* slab, f32x2 v, float vsc) {
   if constexpr (G::MODE == AZ_CONV_FP16X2) {
     const f32x2 vs = v * vsc;  // exact: a power of two
     const f16x2 hi = __builtin_convertvector(vs, f16x2);
+#if AZ_W4_PK
+    // lo = RN16(vs - hi) per element by the mixed-precision FMA (hi read as f16, vs - hi
+    // exact in f32, rounded once to f16): two v_fma_mix*_f16 instead of two f16 -> f32
+    // conversions, the subtraction and a second packed conversion; bit-identical
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(lo)
+        : "v"(__builtin_bit_cast(uint32_t, hi)), "v"(vs.x), "v"(vs.y));
+    *reinterpret_cast<f16x2*>(slab) = hi;
+    *reinterpret_cast<uint32_t*>(slab + G::SLAB) = lo;
+#else
     const f16x2 lo = __builtin_convertvector(vs - __builtin_convertvector(hi, f32x2), f16x2);
     *reinterpret_cast<f16x2*>(slab) = hi;
     *reinterpret_cast<f16x2*>(slab + G::SLAB) = lo;
+#endif
   } else if constexpr (G::MODE == AZ_CONV_SPLIT3) {
     const bf16x2 x0 = __builtin_convertvector(v, bf16x2);
     const f32x2 r1 = v - __builtin_convertvector(x0, f32x2);
@@ -412,36 +462,45 @@ __device__ __forceinline__ void put_point(char* buf, const f32x2 (&rk)[4], int s
 // constant so every update is straight-line register arithmetic
 template <class G, int K>
 __device__ __forceinline__ void fold(f32x16 (&acc)[4][G::NRT], f32x16 (&Y)[2][2][G::NRT]) {
+  // element pairs (e, e + 1) as f32x2: v_pk_add_f32 on the aligned register pairs, the
+  // same IEEE sums element by element
+  auto get = [](const f32x16& v, int e) { return f32x2{v[e], v[e + 1]}; };
+  auto set = [](f32x16& v, int e, f32x2 x) {
+    v[e] = x.x;
+    v[e + 1] = x.y;
+  };
+  auto sub = [](f32x2 a, f32x2 b) { return pk_sub(a, b); };
 #pragma unroll
   for (int t = 0; t < G::NRT; ++t)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const float m0 = acc[0][t][e], m1 = acc[1][t][e], m2 = acc[2][t][e], m3 = acc[3][t][e];
-      const float t0 = (m0 + m1) + m2, t1 = (m1 - m2) - m3;
+    for (int e = 0; e < 16; e += 2) {
+      const f32x2 m0 = get(acc[0][t], e), m1 = get(acc[1][t], e), m2 = get(acc[2][t], e),
+                  m3 = get(acc[3][t], e);
+      const f32x2 t0 = (m0 + m1) + m2, t1 = sub(sub(m1, m2), m3);
       if constexpr (K == 0 && G::NG == 4) {
-        Y[0][0][t][e] = t0;
-        Y[0][1][t][e] = t1;
+        set(Y[0][0][t], e, t0);
+        set(Y[0][1][t], e, t1);
       } else if constexpr (K == 0) {  // NG = 1: Y starts at zero (rows of other workgroups)
-        Y[0][0][t][e] += t0;
-        Y[0][1][t][e] += t1;
+        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
+        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
       } else if constexpr (K == 1) {
-        Y[0][0][t][e] += t0;
-        Y[0][1][t][e] += t1;
+        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
+        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
         if constexpr (G::NG == 4) {
-          Y[1][0][t][e] = t0;
-          Y[1][1][t][e] = t1;
+          set(Y[1][0][t], e, t0);
+          set(Y[1][1][t], e, t1);
         } else {
-          Y[1][0][t][e] += t0;
-          Y[1][1][t][e] += t1;
+          set(Y[1][0][t], e, get(Y[1][0][t], e) + t0);
+          set(Y[1][1][t], e, get(Y[1][1][t], e) + t1);
         }
       } else if constexpr (K == 2) {
-        Y[0][0][t][e] += t0;
-        Y[0][1][t][e] += t1;
-        Y[1][0][t][e] -= t0;
-        Y[1][1][t][e] -= t1;
+        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
+        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
+        set(Y[1][0][t], e, sub(get(Y[1][0][t], e), t0));
+        set(Y[1][1][t], e, sub(get(Y[1][1][t], e), t1));
       } else {
-        Y[1][0][t][e] -= t0;
-        Y[1][1][t][e] -= t1;
+        set(Y[1][0][t], e, sub(get(Y[1][0][t], e), t0));
+        set(Y[1][1][t], e, sub(get(Y[1][1][t], e), t1));
       }
     }
   // materialise Y here: otherwise the compiler sinks the fold arithmetic past the next
@@ -528,7 +587,7 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // KR / KS: the transform-grid rows of chunks v+1 (whose rows are combined here) and v+2
 // (whose windows are read at the end), when known at compile time (AZ_W4_DIET); -1 = from
 // the chunk map at run time
-template <class G, int PAR, int STAGE, int KR = -1, int KS = -1>
+template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
   W4C_STAMP(v, 0);
@@ -554,7 +613,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     if (!(AZ_W4_EXP & 4)) {
       if (AZ_W4_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int t = 0; t < G::NRT; ++t) mma<G>(S.acc[l][t], S.af[t], S.bf[slot]);
+      for (int t = 0; t < G::NRT; ++t) mma<G, FIRST>(S.acc[l][t], S.af[t], S.bf[slot]);
       if (AZ_W4_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
     if (l == 0 && !(AZ_W4_EXP & 2)) {
@@ -568,7 +627,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
           combine_rows(S.rk[u], S.dr[u], Lr);
       }
     }
-    if (!(AZ_W4_EXP & 1)) {
+    if (!(AZ_W4_EXP & 1) && (!(AZ_W4_EXP & 32) || S.tid < 256)) {
       if constexpr (AZ_W4_DIET)
         load_b<G>(S.bf[(slot + G::PD) % G::RING], S.rw, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
       else
@@ -627,6 +686,17 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   }
 }
 
+// groups whose first chunk starts the accumulators itself (mma<G, true>): the whole-K
+// kernel with its first chunk pair peeled (AZ_W4_ZF, default on; 0 = the zeroing pass).
+// Not split3: its six-product body grew and measured 15 % slower peeled (63 -> 73 us)
+#ifndef AZ_W4_ZF
+#define AZ_W4_ZF 1
+#endif
+template <class G>
+constexpr bool zero_free() {
+  return AZ_W4_ZF && AZ_W4_DIET && !G::SPLIT && G::NC >= 4 && G::MODE != AZ_CONV_SPLIT3;
+}
+
 template <class G>
 __device__ __forceinline__ void zero_acc(St<G>& S) {
 #pragma unroll
@@ -644,10 +714,22 @@ __device__ __forceinline__ void run_group(St<G>& S) {
   constexpr int KV = G::NG == 4 ? K : 0;  // the group's place in this workgroup's sequence
   if constexpr (G::NC == 1) {
     run_chunk<G, KV & 1, STAGE>(S, KV);  // one chunk per group: the parity alternates by group
-  } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
+  } else if constexpr (zero_free<G>()) {
     // the whole-K kernel: chunks v = 8K + c; the rows combined in chunk v are chunk v+1's,
     // the windows read at its end chunk v+2's -- both in group K except in the last pair,
-    // peeled so every group index is a compile-time constant
+    // peeled so every group index is a compile-time constant; the first pair peeled too,
+    // its first chunk's products starting the accumulators from C = 0
+    constexpr int KN = K + 1;
+    run_chunk<G, 0, STAGE, K, K, true>(S, KV * G::NC);
+    run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + 1);
+#pragma unroll 1
+    for (int c = 2; c < G::NC - 2; c += 2) {
+      run_chunk<G, 0, STAGE, K, K>(S, KV * G::NC + c);
+      run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + c + 1);
+    }
+    run_chunk<G, 0, STAGE, K, KN>(S, KV * G::NC + G::NC - 2);
+    run_chunk<G, 1, STAGE, KN, KN>(S, KV * G::NC + G::NC - 1);
+  } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
     constexpr int KN = K + 1;
 #pragma unroll 1
     for (int c = 0; c < G::NC - 2; c += 2) {
@@ -664,7 +746,7 @@ __device__ __forceinline__ void run_group(St<G>& S) {
     }
   }
   fold<G, K>(S.acc, S.Y);
-  zero_acc<G>(S);
+  if constexpr (!zero_free<G>()) zero_acc<G>(S);
 }
 
 template <class G>
@@ -878,7 +960,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   }
   lds_barrier();
 
-  zero_acc<G>(S);
+  if constexpr (!zero_free<G>()) zero_acc<G>(S);
   read_a<G>(S.af, S.lds, 0, S.aoff);
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u)
