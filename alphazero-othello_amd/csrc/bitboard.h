@@ -135,10 +135,10 @@ AZ_HD void shl_shr(uint64_t a, uint64_t b, uint64_t& l, uint64_t& r) {
 #endif
 }
 
-// Candidate moves of P through masked opponent stones M along +D and -D: occluded fill
-// with propagator doubling (1 + 1 + 2 + 2 steps cover the six possible run lengths).
+// Candidate moves of P through masked opponent stones M along +D (l) and -D (r): occluded
+// fill with propagator doubling (1 + 1 + 2 + 2 steps cover the six possible run lengths).
 template <int D>
-AZ_HD uint64_t moves_dir(uint64_t P, uint64_t M) {
+AZ_HD void moves_dir2(uint64_t P, uint64_t M, uint64_t& l, uint64_t& r) {
   using namespace tt;
   uint64_t sl, sr;
   shl_shr<D>(P, P, sl, sr);
@@ -155,8 +155,14 @@ AZ_HD uint64_t moves_dir(uint64_t P, uint64_t M) {
   shl_shr<2 * D>(fl, fr, sl, sr);
   fl = bop3<A | (B & C)>(fl, ml, sl);
   fr = bop3<A | (B & C)>(fr, mr, sr);
-  shl_shr<D>(fl, fr, sl, sr);
-  return sl | sr;
+  shl_shr<D>(fl, fr, l, r);
+}
+
+template <int D>
+AZ_HD uint64_t moves_dir(uint64_t P, uint64_t M) {
+  uint64_t l, r;
+  moves_dir2<D>(P, M, l, r);
+  return l | r;
 }
 
 // Horizontal moves by carry propagation: a run of opponent stones (columns 1..6, so no
@@ -168,15 +174,30 @@ AZ_HD uint64_t moves_row_up(uint64_t P, uint64_t I) {
   return (s + I) & ~I;  // landing squares (filtered by `empty` by the caller)
 }
 
+// moves_row_up without the final & ~I: the carry word keeps the opponent stones of runs
+// that did not start at an own stone, and the caller's `empty` mask removes them (and the
+// carries that land on an occupied square) anyway
+AZ_HD uint64_t carries_row_up(uint64_t P, uint64_t I) {
+  const uint64_t s = (P << 1) & I;
+  return s + I;
+}
+
 // Legal placements for `own` against `opp` (the rule of reference envs/othello.py:157-166).
 AZ_HD uint64_t legal(uint64_t own, uint64_t opp) {
   using namespace tt;
   const uint64_t inner = opp & kInner;
-  const uint64_t row =
-      moves_row_up(own, inner) | rev64(moves_row_up(rev64(own), rev64(opp) & kInner));
-  const uint64_t m =
-      bop3<A | B | C>(row, moves_dir<8>(own, opp), moves_dir<7>(own, inner)) |
-      moves_dir<9>(own, inner);
+  // eight candidate words (row up / down, three direction pairs) merged by three bop3 and
+  // an or, the empty-square mask by a fourth bop3 (round 3: 8 VALU fewer than or-ing each
+  // pair first and masking each row word; same-box k_step2 0.1290 vs 0.1293 ms)
+  const uint64_t up = carries_row_up(own, inner);
+  const uint64_t dn = rev64(carries_row_up(rev64(own), rev64(opp) & kInner));
+  uint64_t l8, r8, l7, r7, l9, r9;
+  moves_dir2<8>(own, opp, l8, r8);
+  moves_dir2<7>(own, inner, l7, r7);
+  moves_dir2<9>(own, inner, l9, r9);
+  const uint64_t m1 = bop3<A | B | C>(up, dn, l8);
+  const uint64_t m2 = bop3<A | B | C>(r8, l7, r7);
+  const uint64_t m = bop3<A | B | C>(m1, m2, l9) | r9;
   return bop3<C & ~(A | B)>(own, opp, m);
 }
 
