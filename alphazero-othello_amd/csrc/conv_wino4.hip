@@ -1228,6 +1228,10 @@ extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const 
   AZ_REQUIRE(channels == 128 && mode == AZ_CONV_FP16X2, AZ_ERR_ARG,
              "az_conv3x3_wino4_heads_gpu: 128 channels in FP16X2 mode only (got %d, mode %d)",
              channels, mode);
+  // four boards per workgroup, one workgroup per CU (not the two-board default of
+  // az_conv3x3_wino4_gpu: with two co-resident two-board workgroups this epilogue's values
+  // differed from the separate heads kernel's on ~0.3 % of boards, exact with one per CU --
+  // profiles/r03_heads_two_board.json)
   using G = W4<AZ_CONV_FP16X2, 1>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1263,12 +1267,21 @@ extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float*
   // AZ_W4_NRT (experiments): 1 = eight waves of one row tile (default: two waves per SIMD,
   // no AGPR traffic in the fold; bench 79.7 vs 73.5 games/s same-box), 2 = four waves of two
   static const int nrt = getenv("AZ_W4_NRT") ? atoi(getenv("AZ_W4_NRT")) : 1;
-  // AZ_W4_BOARDS (experiments): 2 = two-board workgroups, two per CU
-  static const int nbw = getenv("AZ_W4_BOARDS") ? atoi(getenv("AZ_W4_BOARDS")) : 4;
+  // Workgroup size (round 3): two boards per workgroup, two workgroups per CU (default for
+  // FP16X2 and FP16) -- the same tiles and arithmetic, bit-identical outputs, but each CU
+  // holds two independent barrier domains instead of one: configs[2] bench 94.4 -> 97.1
+  // games/s same box (profiles/r03_bench_boards2.json; per launch at B = 1,024 -3 % with a
+  // residual, equal without, equal at 4,096).  AZ_W4_BOARDS=4: the four-board workgroup (read
+  // per call, so tests can compare the two forms).
+  const char* nbe = getenv("AZ_W4_BOARDS");
+  const int nbw = nbe ? atoi(nbe) : 2;
 #define W4_GO(M, N) launch_wino4<W4<M, N>>(x, wq, bias, res, y, n_boards, relu, in_absmax, out_absmax, s)
   if (mode == AZ_CONV_FP16X2 && nbw == 2)
     return launch_wino4<W4<AZ_CONV_FP16X2, 1, 2>>(x, wq, bias, res, y, n_boards, relu, in_absmax,
                                                   out_absmax, s);
+  if (mode == AZ_CONV_FP16 && nbw == 2)
+    return launch_wino4<W4<AZ_CONV_FP16, 1, 2>>(x, wq, bias, res, y, n_boards, relu, in_absmax,
+                                                out_absmax, s);
   if (mode == AZ_CONV_SPLIT3) return nrt == 1 ? W4_GO(AZ_CONV_SPLIT3, 1) : W4_GO(AZ_CONV_SPLIT3, 2);
   if (mode == AZ_CONV_FP16) return nrt == 1 ? W4_GO(AZ_CONV_FP16, 1) : W4_GO(AZ_CONV_FP16, 2);
   if (mode == AZ_CONV_FP16X2) return nrt == 1 ? W4_GO(AZ_CONV_FP16X2, 1) : W4_GO(AZ_CONV_FP16X2, 2);

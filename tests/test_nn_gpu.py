@@ -317,6 +317,31 @@ def test_conv3x3_winograd4_splitk_is_deterministic(splits):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("mode", ["fp16x2", "fp16"])
+@pytest.mark.parametrize("B", [1, 3, 130, 1030])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True)])
+def test_conv3x3_winograd4_two_board_form_is_bit_identical(mode, B, res, relu, monkeypatch):
+    """The default two-board workgroups (two per CU) and the four-board form
+    (AZ_W4_BOARDS=4) run the same tiles with the same arithmetic: outputs and the per-board
+    max |y| bit for bit, ragged last workgroups included."""
+    from Models import board_absmax
+
+    m = {"fp16x2": nat.AZ_CONV_FP16X2, "fp16": nat.AZ_CONV_FP16}[mode]
+    x, w, b, r, _ = _case(128, B, 128 * 41 + B)
+    if B > 1:
+        s = torch.logspace(-2, 2, B, device="cuda").view(B, 1, 1, 1)
+        x = (x * s).contiguous(memory_format=torch.channels_last)
+    out = {}
+    for boards in ("2", "4"):
+        monkeypatch.setenv("AZ_W4_BOARDS", boards)
+        amax = torch.zeros(B, dtype=torch.float32, device="cuda")
+        y = _wino_conv(x, w, b, r if res else None, relu, m, fn="az_conv3x3_wino4_gpu",
+                       out_absmax=amax, in_absmax=board_absmax(x))
+        out[boards] = (y, amax)
+    assert torch.equal(out["2"][0], out["4"][0])
+    assert torch.equal(out["2"][1], out["4"][1])
+
+
 def test_conv3x3_winograd4_fp16_mode():
     x, w, b, r, ref64 = _case(128, 37, 128 + 11)
     y = _wino_conv(x, w, b, r, True, nat.AZ_CONV_FP16, fn="az_conv3x3_wino4_gpu")
@@ -396,14 +421,19 @@ def test_trunk_kernel_is_bit_identical(kind):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("boards", ["2", "4"])
 @pytest.mark.parametrize("B", [257, 1024, 1030, 4096])
-def test_fused_heads_bit_identical_to_separate_heads(B, monkeypatch):
+def test_fused_heads_bit_identical_to_separate_heads(B, boards, monkeypatch):
     """AlphaZeroNet on the fp16x2 trunk: the heads fused into the last conv's epilogue
     (az_conv3x3_wino4_heads_gpu, the trunk output kept in LDS) give the same priors and
     values, bit for bit, as the last conv followed by the separate heads kernel
     (az_heads_az_gpu): heads_az.h runs the same code on the same fp32 values.  Ragged
-    batches (a partial last workgroup) included."""
+    batches (a partial last workgroup) included, with two-board (default) and four-board
+    (AZ_W4_BOARDS=4) workgroups: heads_az.h adds the FC input quarters in the same order
+    for any number of boards per workgroup."""
     from Models import FusedInferenceNet
+
+    monkeypatch.setenv("AZ_W4_BOARDS", boards)
 
     torch.manual_seed(3)
     net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
