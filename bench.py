@@ -263,7 +263,8 @@ def conv_roofline(sp, device, n_boards):
             fn = nat.lib.az_conv3x3_wino4_gpu
             args += [nat.ptr(work), None]
             refill = lambda: work.copy_(amax)  # noqa: E731
-            kname = (f"k_conv3x3_wino4 (az_conv3x3_wino4_gpu, Winograd F(2x2,3x3), 4 boards "
+            nbw = int(os.environ.get("AZ_W4_BOARDS", "2"))  # the library's default: 2
+            kname = (f"k_conv3x3_wino4 (az_conv3x3_wino4_gpu, Winograd F(2x2,3x3), {nbw} boards "
                      f"per workgroup, {conv.precision})")
         elif algo == "wino":
             fn = nat.lib.az_conv3x3_wino_gpu
@@ -310,7 +311,9 @@ def conv_roofline(sp, device, n_boards):
         algo = getattr(conv, "algo", "direct")
         per_wg = (16 if algo in ("wino", "wino4") else 9) * C * C * \
             {"split3": 3, "fp16x2": 2}.get(conv.precision, 1) * 2
-        wgs = {"wino": (n_boards + 1) // 2, "wino4": (n_boards + 3) // 4}.get(algo, n_boards)
+        nbw = int(os.environ.get("AZ_W4_BOARDS", "2"))
+        wgs = {"wino": (n_boards + 1) // 2,
+               "wino4": (n_boards + nbw - 1) // nbw}.get(algo, n_boards)
         out["l2_weight_stream"] = {"bytes_per_launch": per_wg * wgs,
                                    "achieved_TBps": round(per_wg * wgs / (ms * 1e-3) / 1e12, 2),
                                    "peak_TBps": L2_PEAK_TBPS}

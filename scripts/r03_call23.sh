@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 3, call 23: the default bench line (configs[2], roofline + cpu_baseline) and a
+# rocprofv3 kernel trace of the same bench (k_step2 launches + the steady-state step)
+set -u
+mkdir -p gpurun_out/r03w
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/r03w/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/r03w/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/r03w/steps.log
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; tail -5 "gpurun_out/r03w/$name.log"; exit $rc; fi
+}
+run bench 600 python bench.py
+run prof 500 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p_c3 -o run -- python3 bench.py --skip-cpu --steps 2000 --warmup 24000
+cp /tmp/p_c3/run_kernel_stats.csv gpurun_out/r03w/kernel_stats.csv
+run tail 120 python scripts/trace_tail.py /tmp/p_c3/run_kernel_trace.csv 2000
+exit 0
