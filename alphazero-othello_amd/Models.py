@@ -599,6 +599,8 @@ class FusedInferenceNet(nn.Module, Inference):
             fuse = (heads_into is not None and not sk and self.fuse_heads
                     and self._fused_heads_ready() and c2s[-1].algo == "wino4"
                     and c2s[-1].precision == "fp16x2" and c2s[-1].channels == 128)
+            if not sk and self._trunk4_ready(c1s, c2s, B):
+                return self._trunk4(h, bufs, c1s, c2s, heads_into if fuse else None)
             for i, (c1, c2) in enumerate(zip(c1s, c2s)):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)
                 if fuse and i == len(c1s) - 1:
@@ -611,6 +613,53 @@ class FusedInferenceNet(nn.Module, Inference):
         for c1, c2 in zip(c1s, c2s):
             h = c2(c1(h), res=h)
         return h
+
+    # fp16x2 tower as one persistent launch (az_trunk_wino4_gpu): every block conv but a
+    # fused-heads last one in a single kernel, each two-board workgroup carrying its boards
+    # through the layers -- bit-identical to the per-layer launches.  Used while every
+    # workgroup is resident at once (two two-board workgroups per CU: B <= 4 x CUs, e.g.
+    # configs[2]'s 1,024): configs[2] 97.5 -> 98.0 games/s same box; at 4,096 boards (four
+    # rounds of workgroups, each at its own layer, so the layers' weights compete for L2) it
+    # measured 1.6 % slower (profiles/r03_trunk4_ab.json).  AZ_FUSE_TRUNK4=0: off.
+    fuse_trunk4 = os.environ.get("AZ_FUSE_TRUNK4", "1") != "0"
+
+    def _trunk4_ready(self, c1s, c2s, B):
+        convs = c1s + c2s
+        if not (self.fuse_trunk4 and convs and os.environ.get("AZ_W4_BOARDS", "2") == "2"):
+            return False
+        dev = convs[0].wq.device
+        if B > 4 * torch.cuda.get_device_properties(dev).multi_processor_count:
+            return False
+        if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16x2"
+                   and c.channels == 128 for c in convs):
+            return False
+        if not hasattr(self, "_t4"):
+            order = [c for pair in zip(c1s, c2s) for c in pair]  # layer order
+            self._t4 = {
+                "wq": torch.tensor([c.wq.data_ptr() for c in order], dtype=torch.int64, device=dev),
+                "bias": torch.tensor([c.bias.data_ptr() for c in order], dtype=torch.int64,
+                                     device=dev)}
+        return True
+
+    def _trunk4(self, h, bufs, c1s, c2s, heads_into):
+        """The tower on az_trunk_wino4_gpu: all 2n convs (returns the output), or with
+        heads_into the first 2n - 1 and the last conv with the heads fused (returns None)."""
+        import az_native as nat
+
+        B = h.shape[0]
+        n_convs = 2 * len(c1s) - (1 if heads_into is not None else 0)
+        hb = [torch.empty_like(h, memory_format=torch.channels_last) for _ in range(2)]
+        t = torch.empty_like(h, memory_format=torch.channels_last)
+        nat.check(nat.lib.az_trunk_wino4_gpu(
+            nat.ptr(self._t4["wq"]), nat.ptr(self._t4["bias"]), nat.ptr(h), nat.ptr(hb[0]),
+            nat.ptr(hb[1]), nat.ptr(t), nat.ptr(bufs[0]), nat.ptr(bufs[1]), B, n_convs,
+            c1s[0].channels, nat.stream_ptr()), "az_trunk_wino4_gpu")
+        n_blocks = n_convs // 2
+        h_last = hb[(n_blocks - 1) & 1] if n_blocks else h
+        if heads_into is not None:
+            c2s[-1].forward_heads(t, h_last, bufs[1], self._hw, *heads_into)
+            return None
+        return h_last
 
     def _fused_heads_ready(self):
         if self.kind != "az" or self.conv_impl != "hip":

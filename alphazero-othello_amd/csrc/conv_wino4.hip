@@ -842,8 +842,10 @@ __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int
                      live, active, ho.w, L, ho.priors, ho.values);
 }
 
-template <class G, bool RES, bool RELU, bool HEADS = false>
-__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
+// One conv of this workgroup's boards (the whole kernel of k_conv3x3_wino4; the persistent
+// trunk k_trunk_wino4 runs it once per layer on the same boards).
+template <class G, bool RES, bool RELU, bool HEADS = false, bool LAUNDER = false>
+__device__ __forceinline__ void conv_body(
     const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
     float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho) {
@@ -861,7 +863,10 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
     S.rw = __builtin_amdgcn_make_buffer_rsrc((void*)wq, 0, G::QSTEPS * G::STEP_BYTES, 0x00020000);
   }
   S.res = res;
-  const int tid = threadIdx.x;
+  // laundered: the persistent trunk runs this body once per layer, and everything derived
+  // from the lane index hoisted out of its layer loop would stay live across both bodies
+  int tid = threadIdx.x;
+  if constexpr (LAUNDER) asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cb = wave & 3, rt0 = G::NRT == 1 ? wave >> 2 : 0;
@@ -1043,6 +1048,54 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
   // read its entries in the prologue, before the first barrier)
   if (G::SCALED && !G::SPLIT && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
   W4_STAMP(6);
+  }
+}
+
+template <class G, bool RES, bool RELU, bool HEADS = false>
+__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
+    const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
+    const float* __restrict__ res, float* __restrict__ y, int n_boards,
+    float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho) {
+  conv_body<G, RES, RELU, HEADS>(x, wq, bias, res, y, n_boards, in_absmax, out_absmax, ho);
+}
+
+// Persistent trunk (az_trunk_wino4_gpu): a workgroup runs n_convs consecutive 3x3 convs of
+// the residual tower on ITS boards -- conv 2i: relu(conv(h)) -> t, conv 2i+1: relu(conv(t) +
+// h) -> the other block buffer -- so no layer waits for another workgroup and the 8-9
+// kernel boundaries (launch gap + the slowest workgroup's tail, each layer) go.  Every
+// activation a layer reads was written by this workgroup, so a barrier with its stores
+// drained (vmcnt(0)) and an L1 invalidate (buffer_inv sc0: the ping-pong buffers were read
+// by earlier layers) order it; per-board ranges ping-pong amax[0] / amax[1] as between the
+// per-layer launches.  Same arithmetic per layer: bit-identical to those launches.
+struct TrunkW4 {
+  const char* const* wq;     // [n_convs] prepared weights (layer order)
+  const float* const* bias;  // [n_convs]
+  const float* h_in;         // block input (the stem's output), not written
+  float* hb[2];              // block outputs, ping-pong
+  float* t;                  // conv1 outputs
+  float* amax[2];            // per-board ranges: amax[0] = h_in's on entry
+  int n_boards, n_convs;
+};
+
+__device__ __forceinline__ void layer_fence() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\tbuffer_inv sc0" ::: "memory");
+}
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a) {
+  const float* h = a.h_in;
+  int ob = 0;
+  for (int i = 0; i < a.n_convs; ++i) {
+    if (i > 0) layer_fence();
+    if ((i & 1) == 0) {
+      conv_body<G, false, true, false, true>(h, a.wq[i], a.bias[i], nullptr, a.t, a.n_boards, a.amax[0],
+                                a.amax[1], HeadsOut{});
+    } else {
+      conv_body<G, true, true, false, true>(a.t, a.wq[i], a.bias[i], h, a.hb[ob], a.n_boards, a.amax[1],
+                               a.amax[0], HeadsOut{});
+      h = a.hb[ob];
+      ob ^= 1;
+    }
   }
 }
 
@@ -1245,6 +1298,37 @@ extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const 
                      (size_t)G::LDS_BYTES, azc::as_stream(stream), x,
                      static_cast<const char*>(wq), bias, res, nullptr, n_boards, in_absmax,
                      nullptr, ho);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias,
+                                  const float* h_in, float* hb0, float* hb1, float* t,
+                                  float* amax0, float* amax1, int32_t n_boards, int32_t n_convs,
+                                  int32_t channels, void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && n_convs >= 0, AZ_ERR_ARG, "az_trunk_wino4_gpu: negative size");
+  if (n_boards == 0 || n_convs == 0) return AZ_OK;
+  AZ_REQUIRE(wq && bias && h_in && hb0 && hb1 && t && amax0 && amax1, AZ_ERR_ARG,
+             "az_trunk_wino4_gpu: null buffer");
+  AZ_REQUIRE(h_in != hb0 && h_in != hb1 && h_in != t && hb0 != hb1 && hb0 != t && hb1 != t &&
+                 amax0 != amax1,
+             AZ_ERR_ARG, "az_trunk_wino4_gpu: aliased buffers");
+  AZ_REQUIRE(((uintptr_t)h_in | (uintptr_t)hb0 | (uintptr_t)hb1 | (uintptr_t)t) % 16 == 0,
+             AZ_ERR_ARG, "az_trunk_wino4_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(channels == 128, AZ_ERR_ARG, "az_trunk_wino4_gpu: channels must be 128, got %d",
+             channels);
+  using G = W4<AZ_CONV_FP16X2, 1, 2>;  // two-board workgroups, FP16X2
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  const TrunkW4 a{reinterpret_cast<const char* const*>(wq), bias, h_in, {hb0, hb1}, t,
+                  {amax0, amax1}, n_boards, n_convs};
+  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  hipLaunchKernelGGL((k_trunk_wino4<G>), dim3(grid), dim3(G::THREADS), (size_t)G::LDS_BYTES,
+                     azc::as_stream(stream), a);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -421,6 +421,35 @@ def test_trunk_kernel_is_bit_identical(kind):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [257, 1024, 1030, 4096])
+@pytest.mark.parametrize("heads", [True, False])
+def test_persistent_trunk_bit_identical_to_layer_launches(B, heads, monkeypatch):
+    """The fp16x2 tower as one persistent launch (az_trunk_wino4_gpu: each two-board
+    workgroup carries its boards through the layers) against one launch per conv: priors
+    and values (heads fused into the last conv, or the separate heads kernel after the
+    whole tower) and the tower's output, bit for bit, ragged last workgroups included."""
+    from Models import FusedInferenceNet
+
+    torch.manual_seed(5)
+    net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    monkeypatch.setattr(FusedInferenceNet, "fuse_heads", heads)
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    out = {}
+    for flag in (True, False):
+        monkeypatch.setattr(FusedInferenceNet, "fuse_trunk4", flag)
+        pr = torch.full((B, 65), float("nan"), device="cuda")
+        va = torch.full((B,), float("nan"), device="cuda")
+        with torch.no_grad():
+            fused.evaluate_into(x, pr, va)
+            h = fused._trunk(x.view(B, 1, 8, 8))
+        torch.cuda.synchronize()
+        out[flag] = (pr, va, h)
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+    assert not torch.isnan(out[True][0]).any()
+
+
 @pytest.mark.parametrize("boards", ["2", "4"])
 @pytest.mark.parametrize("B", [257, 1024, 1030, 4096])
 def test_fused_heads_bit_identical_to_separate_heads(B, boards, monkeypatch):
