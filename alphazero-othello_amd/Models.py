@@ -532,6 +532,9 @@ class FusedInferenceNet(nn.Module, Inference):
         evaluate_into(..., stem_done=True) at that batch size then start at the first block."""
         if not (self._fused_heads_ready() and self._stem_stored()):
             return None
+        if self.trunk_stem and self._trunk4_ready(list(self.c1), list(self.c2), B) \
+                and self.splitk_for(B) == 0:
+            return None  # the persistent trunk runs the stem (its output stays in L2)
         ent = self._scratch(device, B)
         ent["pinned"] = True
         C = self.stem.channels
@@ -581,13 +584,6 @@ class FusedInferenceNet(nn.Module, Inference):
             B = x.shape[0]
             ent = self._scratch(x.device, B)
             bufs = ent["absmax"]
-            if stem_done:  # written by the engine's select launch (engine_stem)
-                h = ent["h0"]
-            elif isinstance(self.stem, _HipStem):
-                h = self.stem(x, absmax=bufs[0])
-            else:
-                h = self.stem(x)
-                board_absmax(h, out=bufs[0])
             sk = {}
             splits = self.splitk_for(B)
             if splits and all(c.algo == "wino4" for c in c1s + c2s):
@@ -599,7 +595,18 @@ class FusedInferenceNet(nn.Module, Inference):
             fuse = (heads_into is not None and not sk and self.fuse_heads
                     and self._fused_heads_ready() and c2s[-1].algo == "wino4"
                     and c2s[-1].precision == "fp16x2" and c2s[-1].channels == 128)
-            if not sk and self._trunk4_ready(c1s, c2s, B):
+            t4 = not sk and self._trunk4_ready(c1s, c2s, B)
+            if t4 and not stem_done and isinstance(self.stem, _HipStem):
+                # the stem inside the persistent trunk (each workgroup's boards first)
+                return self._trunk4(None, bufs, c1s, c2s, heads_into if fuse else None, planes=x)
+            if stem_done:  # written by the engine's select launch (engine_stem)
+                h = ent["h0"]
+            elif isinstance(self.stem, _HipStem):
+                h = self.stem(x, absmax=bufs[0])
+            else:
+                h = self.stem(x)
+                board_absmax(h, out=bufs[0])
+            if t4:
                 return self._trunk4(h, bufs, c1s, c2s, heads_into if fuse else None)
             for i, (c1, c2) in enumerate(zip(c1s, c2s)):
                 t = c1(h, in_absmax=bufs[0], out_absmax=bufs[1], **sk)
@@ -622,6 +629,11 @@ class FusedInferenceNet(nn.Module, Inference):
     # rounds of workgroups, each at its own layer, so the layers' weights compete for L2) it
     # measured 1.6 % slower (profiles/r03_trunk4_ab.json).  AZ_FUSE_TRUNK4=0: off.
     fuse_trunk4 = os.environ.get("AZ_FUSE_TRUNK4", "1") != "0"
+    # AZ_TRUNK_STEM=1: the stem too (each workgroup's boards before the first layer) instead
+    # of in the engine's select launch (engine_stem then returns None).  Off: configs[2] 96.4
+    # vs 97.0 games/s with the engine stem, same box (profiles/r03_trunk_stem_ab.json) -- the
+    # stem's 33.5 MB store then precedes the first layer instead of hiding under the descents
+    trunk_stem = os.environ.get("AZ_TRUNK_STEM", "0") == "1"
 
     def _trunk4_ready(self, c1s, c2s, B):
         convs = c1s + c2s
@@ -641,19 +653,28 @@ class FusedInferenceNet(nn.Module, Inference):
                                      device=dev)}
         return True
 
-    def _trunk4(self, h, bufs, c1s, c2s, heads_into):
+    def _trunk4(self, h, bufs, c1s, c2s, heads_into, planes=None):
         """The tower on az_trunk_wino4_gpu: all 2n convs (returns the output), or with
-        heads_into the first 2n - 1 and the last conv with the heads fused (returns None)."""
+        heads_into the first 2n - 1 and the last conv with the heads fused (returns None).
+        planes (canonical boards [B, 1, 8, 8]) instead of h: the stem runs in the same launch."""
         import az_native as nat
 
+        C = c1s[0].channels
+        if planes is not None:
+            B = planes.shape[0]
+            planes = planes.reshape(B, 64).contiguous()
+            h = torch.empty((B, C, 8, 8), dtype=torch.float32, device=planes.device,
+                            memory_format=torch.channels_last)
         B = h.shape[0]
         n_convs = 2 * len(c1s) - (1 if heads_into is not None else 0)
         hb = [torch.empty_like(h, memory_format=torch.channels_last) for _ in range(2)]
         t = torch.empty_like(h, memory_format=torch.channels_last)
+        st = self.stem if planes is not None else None
         nat.check(nat.lib.az_trunk_wino4_gpu(
-            nat.ptr(self._t4["wq"]), nat.ptr(self._t4["bias"]), nat.ptr(h), nat.ptr(hb[0]),
-            nat.ptr(hb[1]), nat.ptr(t), nat.ptr(bufs[0]), nat.ptr(bufs[1]), B, n_convs,
-            c1s[0].channels, nat.stream_ptr()), "az_trunk_wino4_gpu")
+            nat.ptr(self._t4["wq"]), nat.ptr(self._t4["bias"]), nat.ptr(planes),
+            nat.ptr(st.w9) if st is not None else None, nat.ptr(st.bias) if st is not None else None,
+            nat.ptr(h), nat.ptr(hb[0]), nat.ptr(hb[1]), nat.ptr(t), nat.ptr(bufs[0]),
+            nat.ptr(bufs[1]), B, n_convs, C, nat.stream_ptr()), "az_trunk_wino4_gpu")
         n_blocks = n_convs // 2
         h_last = hb[(n_blocks - 1) & 1] if n_blocks else h
         if heads_into is not None:

@@ -1070,10 +1070,13 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
 struct TrunkW4 {
   const char* const* wq;     // [n_convs] prepared weights (layer order)
   const float* const* bias;  // [n_convs]
-  const float* h_in;         // block input (the stem's output), not written
+  float* h_in;               // block input (the stem's output): written only with `planes`
   float* hb[2];              // block outputs, ping-pong
   float* t;                  // conv1 outputs
-  float* amax[2];            // per-board ranges: amax[0] = h_in's on entry
+  float* amax[2];            // per-board ranges: amax[0] = h_in's (on entry, or the stem's)
+  const float* planes;       // optional: the stem's inputs [n][64] (h_in computed here)
+  const float* stem_w;       // [9][C]
+  const float* stem_b;       // [C]
   int n_boards, n_convs;
 };
 
@@ -1081,18 +1084,76 @@ __device__ __forceinline__ void layer_fence() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\tbuffer_inv sc0" ::: "memory");
 }
 
+// The stem (Ci = 1 -> C = 128, 3x3, bias, ReLU) of board b by a 256-thread workgroup, and the
+// board's max |y|: k_conv_stem's (conv.hip) thread mapping, tap order and fmaf chain, so the
+// outputs are bit-identical to that kernel's (and to the engine stem's).  s_pl / s_max: LDS.
+__device__ __forceinline__ void stem_board(const float* __restrict__ planes,
+                                           const float* __restrict__ w,
+                                           const float* __restrict__ bias, float* __restrict__ y,
+                                           float* __restrict__ absmax, int b, float* s_pl,
+                                           float* s_max) {
+  constexpr int CO = 128, G4 = CO / 4, PPI = 256 / G4;
+  const int tid = threadIdx.x;
+  const int co = (tid % G4) * 4;
+  float4 wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = *reinterpret_cast<const float4*>(w + t * CO + co);
+  const float4 bv = *reinterpret_cast<const float4*>(bias + co);
+  __syncthreads();  // the previous board's planes and maxima are no longer read
+  if (tid < 64) s_pl[tid] = planes[(size_t)b * 64 + tid];
+  __syncthreads();
+  float4* out = reinterpret_cast<float4*>(y + (size_t)b * 64 * CO);
+  float bmax = 0.0f;
+#pragma unroll
+  for (int p0 = 0; p0 < 64; p0 += PPI) {
+    const int p = p0 + tid / G4, py = p >> 3, px = p & 7;
+    float4 acc = bv;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+      if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
+        const float v = s_pl[yy * 8 + xx];
+        acc.x = fmaf(v, wv[t].x, acc.x);
+        acc.y = fmaf(v, wv[t].y, acc.y);
+        acc.z = fmaf(v, wv[t].z, acc.z);
+        acc.w = fmaf(v, wv[t].w, acc.w);
+      }
+    }
+    acc.x = fmaxf(acc.x, 0.f);
+    acc.y = fmaxf(acc.y, 0.f);
+    acc.z = fmaxf(acc.z, 0.f);
+    acc.w = fmaxf(acc.w, 0.f);
+    out[p * G4 + co / 4] = acc;
+    bmax = fmaxf(bmax, fmaxf(fmaxf(acc.x, acc.y), fmaxf(acc.z, acc.w)));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, off, 64));
+  if ((tid & 63) == 0) s_max[tid >> 6] = bmax;
+  __syncthreads();
+  if (tid == 0) absmax[b] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+}
+
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a) {
+  if (a.planes) {  // the stem of this workgroup's boards first (its output never leaves L2)
+    static_assert(G::THREADS == 256 && G::C == 128, "stem_board's mapping");
+    extern __shared__ float4 lds4[];
+    float* sp = reinterpret_cast<float*>(lds4);
+    const int b0 = blockIdx.x * G::BOARDS;
+    for (int bd = 0; bd < G::BOARDS && b0 + bd < a.n_boards; ++bd)
+      stem_board(a.planes, a.stem_w, a.stem_b, a.h_in, a.amax[0], b0 + bd, sp, sp + 64);
+    layer_fence();
+  }
   const float* h = a.h_in;
   int ob = 0;
   for (int i = 0; i < a.n_convs; ++i) {
     if (i > 0) layer_fence();
     if ((i & 1) == 0) {
-      conv_body<G, false, true, false, true>(h, a.wq[i], a.bias[i], nullptr, a.t, a.n_boards, a.amax[0],
-                                a.amax[1], HeadsOut{});
+      conv_body<G, false, true, false, true>(h, a.wq[i], a.bias[i], nullptr, a.t, a.n_boards,
+                                             a.amax[0], a.amax[1], HeadsOut{});
     } else {
-      conv_body<G, true, true, false, true>(a.t, a.wq[i], a.bias[i], h, a.hb[ob], a.n_boards, a.amax[1],
-                               a.amax[0], HeadsOut{});
+      conv_body<G, true, true, false, true>(a.t, a.wq[i], a.bias[i], h, a.hb[ob], a.n_boards,
+                                            a.amax[1], a.amax[0], HeadsOut{});
       h = a.hb[ob];
       ob ^= 1;
     }
@@ -1303,12 +1364,14 @@ extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const 
 }
 
 extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias,
-                                  const float* h_in, float* hb0, float* hb1, float* t,
-                                  float* amax0, float* amax1, int32_t n_boards, int32_t n_convs,
-                                  int32_t channels, void* stream) {
+                                  const float* planes, const float* stem_w,
+                                  const float* stem_b, float* h_in, float* hb0, float* hb1,
+                                  float* t, float* amax0, float* amax1, int32_t n_boards,
+                                  int32_t n_convs, int32_t channels, void* stream) {
   AZ_REQUIRE(n_boards >= 0 && n_convs >= 0, AZ_ERR_ARG, "az_trunk_wino4_gpu: negative size");
-  if (n_boards == 0 || n_convs == 0) return AZ_OK;
-  AZ_REQUIRE(wq && bias && h_in && hb0 && hb1 && t && amax0 && amax1, AZ_ERR_ARG,
+  if (n_boards == 0 || (n_convs == 0 && !planes)) return AZ_OK;
+  AZ_REQUIRE((n_convs == 0 || (wq && bias)) && h_in && hb0 && hb1 && t && amax0 && amax1,
+             AZ_ERR_ARG,
              "az_trunk_wino4_gpu: null buffer");
   AZ_REQUIRE(h_in != hb0 && h_in != hb1 && h_in != t && hb0 != hb1 && hb0 != t && hb1 != t &&
                  amax0 != amax1,
@@ -1317,6 +1380,8 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
              AZ_ERR_ARG, "az_trunk_wino4_gpu: buffers must be 16-byte aligned");
   AZ_REQUIRE(channels == 128, AZ_ERR_ARG, "az_trunk_wino4_gpu: channels must be 128, got %d",
              channels);
+  AZ_REQUIRE(!planes || (stem_w && stem_b && ((uintptr_t)stem_w | (uintptr_t)stem_b) % 16 == 0),
+             AZ_ERR_ARG, "az_trunk_wino4_gpu: planes without 16-byte aligned stem weights");
   using G = W4<AZ_CONV_FP16X2, 1, 2>;  // two-board workgroups, FP16X2
   static bool attr_set = false;
   if (!attr_set) {
@@ -1325,7 +1390,7 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
     attr_set = true;
   }
   const TrunkW4 a{reinterpret_cast<const char* const*>(wq), bias, h_in, {hb0, hb1}, t,
-                  {amax0, amax1}, n_boards, n_convs};
+                  {amax0, amax1}, planes, stem_w, stem_b, n_boards, n_convs};
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
   hipLaunchKernelGGL((k_trunk_wino4<G>), dim3(grid), dim3(G::THREADS), (size_t)G::LDS_BYTES,
                      azc::as_stream(stream), a);

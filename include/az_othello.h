@@ -426,14 +426,18 @@ int az_trunk_wino_gpu(const float* planes, const float* stem_w, const float* ste
  * block's output in hb0) -- with az_conv3x3_wino4_gpu's arithmetic per layer (bit-identical
  * to those launches), no grid-wide barrier (a conv mixes positions within a board only).
  * h_in [n][64][128] NHWC = the stem output (read only); amax0 = its per-board max |x| on
- * entry, amax1 zeros; on return the ranges of the last output are in amax1 (n_convs odd:
+ * entry, amax1 zeros.  With planes (float [n][64], the canonical boards) and the stem's
+ * stem_w [9][128] / stem_b [128], the kernel first runs the stem on each workgroup's boards
+ * (az_conv_stem_gpu's arithmetic, bit-identical) into h_in and amax0 (then written, and
+ * n_convs may be 0); on return the ranges of the last output are in amax1 (n_convs odd:
  * t) or amax0 (even: the last block output), the other zeroed.  wq / bias: device arrays of
  * n_convs device pointers (az_conv3x3_wino_prep_gpu FP16X2 weights, fp32 biases) in layer
  * order.  Replaces reference Models.py:209-210 (AlphaZeroNet.forward's res tower); an odd
  * n_convs leaves the last block's second conv to az_conv3x3_wino4_heads_gpu. */
-int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias, const float* h_in,
-                       float* hb0, float* hb1, float* t, float* amax0, float* amax1,
-                       int32_t n_boards, int32_t n_convs, int32_t channels, void* stream);
+int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias, const float* planes,
+                       const float* stem_w, const float* stem_b, float* h_in, float* hb0,
+                       float* hb1, float* t, float* amax0, float* amax1, int32_t n_boards,
+                       int32_t n_convs, int32_t channels, void* stream);
 
 /* ---------------- replay buffer (device) -------------------------------------------
  * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with

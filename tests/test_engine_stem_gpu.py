@@ -95,7 +95,12 @@ def _net():
     return AlphaZeroNet(8, 65, 5, 128)
 
 
-def test_evaluate_into_with_engine_stem_is_bit_identical():
+def test_evaluate_into_with_engine_stem_is_bit_identical(monkeypatch):
+    """The stem in the select launch (engine stem), the stem kernel and the stem inside the
+    persistent trunk (az_trunk_wino4_gpu with planes) give the same priors and values."""
+    from Models import FusedInferenceNet
+
+    monkeypatch.setattr(FusedInferenceNet, "trunk_stem", False)  # the engine stem on
     sp = BatchedSelfPlay(_net(), ARGS, 512, seed=3, use_graph=False, d4_augment=True)
     assert sp.engine_stem and sp.net.precision == "fp16x2"
     sp.reset(start_budget=-1, stagger_steps=30)
@@ -109,14 +114,25 @@ def test_evaluate_into_with_engine_stem_is_bit_identical():
         p0 = torch.empty_like(e.priors)
         v0 = torch.empty_like(e.values)
         sp.net.evaluate_into(e.nn_in.clone(), p0, v0)
+        monkeypatch.setattr(FusedInferenceNet, "trunk_stem", True)
+        p2 = torch.empty_like(e.priors)
+        v2 = torch.empty_like(e.values)
+        sp.net.evaluate_into(e.nn_in.clone(), p2, v2)
     torch.cuda.synchronize()
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
+    assert torch.equal(p0, p2) and torch.equal(v0, v2)
     assert torch.isfinite(p1).all() and torch.isfinite(v1).all()
 
 
-def test_selfplay_with_and_without_engine_stem_same_games():
+@pytest.mark.parametrize("trunk_stem", [False, True])
+def test_selfplay_with_and_without_engine_stem_same_games(trunk_stem, monkeypatch):
+    """Self-play with the stem in the select launch against the stem elsewhere (its own
+    kernel, or -- trunk_stem -- inside the persistent trunk launch): the same games."""
+    from Models import FusedInferenceNet
+
     runs = []
     for on in (True, False):
+        monkeypatch.setattr(FusedInferenceNet, "trunk_stem", trunk_stem and not on)
         sp = BatchedSelfPlay(_net(), ARGS, 512, seed=8, engine_stem=on, require_graph=True,
                              sample_capacity=512 * 200)
         assert sp.engine_stem == on
