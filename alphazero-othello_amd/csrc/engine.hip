@@ -608,11 +608,19 @@ __device__ __forceinline__ void move_body(const Params& p, int q, int deferred, 
 // move phase of the previous step's list (par ^ 1) while the others descend; a slot whose
 // move is in that list is skipped (nothing of it is read: k_move writes it concurrently, and
 // those writes become visible at the launch boundary) and plays again next step.
-template <int KMAX, bool MERGED = false>
+// FUSED (az_select_move_expand; deferred moves only): each slot's wave first expands and backs
+// up the previous step's waiting leaves (expand_slot on priors / values, the evaluation that
+// step's net wrote), then descends -- one launch per step instead of select + expand.  A
+// search those leaves complete joins this step's move list (moved by the next launch) and
+// the slot sits this step out, so each of its moves lands one step later than with k_expand;
+// which step a move lands in never changes a game.
+template <int KMAX, bool MERGED = false, bool FUSED = false>
 __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restrict__ nn_in,
                                                       int32_t* __restrict__ leaf_o,
                                                       int max_descents, int par,
-                                                      int move_blocks) {
+                                                      int move_blocks,
+                                                      const float* __restrict__ priors,
+                                                      const float* __restrict__ values) {
   if constexpr (MERGED) {  // a separate instantiation: the plain one keeps its registers
     if ((int)blockIdx.x < move_blocks) {
       move_body(p, par ^ 1, 1, move_blocks, (int)blockIdx.x);
@@ -636,6 +644,14 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       emit_none_rows(p, nn_in, leaf_o, row0, K);
       return;
     }
+  }
+  if constexpr (FUSED) {
+    if (expand_slot<KMAX>(p, g, priors, values, par, sst)) {
+      emit_none_rows(p, nn_in, leaf_o, row0, K);
+      return;
+    }
+    // the expansion's and backup's stores before this wave's descent loads
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   const int status = p.g.status[g];
   // the stagger schedule counts steps: the engine's, or the slot's own with deferred moves
@@ -967,14 +983,16 @@ __device__ double expand_backup_leaf(const Params& p, int g, int half, const Lea
   return v;
 }
 
-// One wavefront per slot: the slot's waiting leaves in descent order (rows g*K .. g*K+K-1
-// of the evaluation batch, the list ends at the first -1).
+// The expansion of slot g's waiting leaves in descent order (rows g*K .. g*K+K-1 of the
+// evaluation batch, the list ends at the first -1): k_expand's body, also run by the slot's
+// wave at the start of the next select launch (fused expansion, az_select_move_expand).
+// Returns whether the slot's search is complete after them (then pushed to move list `par`
+// with step sst_push; -1 = this launch's step count minus one, the standalone kernel's).
 template <int KMAX>
-__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
-                                                      const float* __restrict__ values,
-                                                      int par) {
-  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
-  if (g >= p.G) return;
+__device__ __forceinline__ bool expand_slot(const Params& p, int g,
+                                            const float* __restrict__ priors,
+                                            const float* __restrict__ values, int par,
+                                            int sst_push) {
   const int K = KMAX == 1 ? 1 : p.K;
   const int64_t row0 = (int64_t)g * K;
   const int lane = lane_id();
@@ -988,7 +1006,6 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < K) in[j] = load_leaf_in(p, row0 + j, priors, values);
-  ENG_STAMP_BEGIN(2);
   // every load above in flight before any is waited for (the compiler would otherwise sink
   // them past the early exit below, one dependent round trip each)
   asm volatile("" ::"v"(half), "v"(n_nodes), "v"(sd0), "v"(target));
@@ -999,8 +1016,7 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
                    "v"(in[j].pr64), "v"(in[j].v), "v"(in[j].sym));
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) in[j].sym = p.d4 ? in[j].sym : 0;
-  if (in[0].leaf < 0) return;
-  ENG_STAMP(2);
+  if (in[0].leaf < 0) return false;
   double done_v[KMAX];
   int n_sims = 0;
 #pragma unroll
@@ -1022,26 +1038,34 @@ __global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __r
     // the next leaf's path loads must see this backup's N/W stores
     if (KMAX > 1) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
+  const int sd = sd0 + n_sims;
   if (lane == 0) {
     p.g.leaf[row0] = -1;
     p.g.n_nodes[g] = n_nodes;
-    const int sd = sd0 + n_sims;
     if (n_sims) {
       p.g.sims_done[g] = sd;
       p.g.sims_acc[g] += (unsigned long long)n_sims;
     }
     if (sd >= target) {
-      if (p.auto_play) push_ready(p, g, par, p.defer ? p.g.sstep[g] - 1 : 0);
-      else p.g.status[g] = kSearchDone;
+      if (p.auto_play)
+        push_ready(p, g, par, sst_push >= 0 ? sst_push : (p.defer ? p.g.sstep[g] - 1 : 0));
+      else
+        p.g.status[g] = kSearchDone;
     }
   }
+  return sd >= target;
+}
+
+// One wavefront per slot: expand_slot.
+template <int KMAX>
+__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
+                                                      const float* __restrict__ values,
+                                                      int par) {
+  const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
+  if (g >= p.G) return;
+  ENG_STAMP_BEGIN(2);
+  expand_slot<KMAX>(p, g, priors, values, par, -1);
   ENG_STAMP(3);
-#if AZ_ENG_STAMP
-  st_[4] = (unsigned long long)in[0].leaf;
-  st_[5] = (unsigned long long)in[0].plen;
-  st_[6] = (unsigned long long)n_nodes;
-  st_[7] = (unsigned long long)g;
-#endif
   ENG_STAMP_END();
 }
 
@@ -2066,6 +2090,19 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
                           (int)e->lds_move) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_select<kMaxLeaves, true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      // ... and with the fused expansion (az_select_move_expand)
+      hipFuncSetAttribute((const void*)k_select<1, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<2, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<4, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)e->lds_move) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_select<kMaxLeaves, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess) {
     (void)hipGetLastError();
   }
@@ -2145,7 +2182,8 @@ int az_begin_search(az_engine* e, int32_t slot, int32_t num_simulations, void* s
 
 // k_select (+ the deferred move phase in its first move_blocks workgroups)
 static int launch_select(az_engine* e, float* nn_in, int32_t* leaf_o, int par, int move_blocks,
-                         hipStream_t s) {
+                         hipStream_t s, const float* priors = nullptr,
+                         const float* values = nullptr, bool fused = false) {
   // Simulations that end on a terminal node need no evaluation and run inside the select
   // call; cap them per step so one end-game tree (every simulation terminal) cannot hold
   // the whole batched step for hundreds of dependent descents.  Host-driven engines step
@@ -2163,12 +2201,15 @@ static int launch_select(az_engine* e, float* nn_in, int32_t* leaf_o, int par, i
   // the kernels' per-leaf arrays sized to the next power of two >= K (registers)
 #define AZ_SEL_GO(KM)                                                                       \
   do {                                                                                     \
-    if (move_blocks)                                                                       \
+    if (fused)                                                                             \
+      hipLaunchKernelGGL((k_select<KM, true, true>), grid, dim3(kSelBlock), lds, s, e->p,   \
+                         nn_in, leaf_o, max_descents, par, move_blocks, priors, values);   \
+    else if (move_blocks)                                                                  \
       hipLaunchKernelGGL((k_select<KM, true>), grid, dim3(kSelBlock), lds, s, e->p, nn_in,  \
-                         leaf_o, max_descents, par, move_blocks);                          \
+                         leaf_o, max_descents, par, move_blocks, nullptr, nullptr);        \
     else                                                                                   \
       hipLaunchKernelGGL((k_select<KM, false>), grid, dim3(kSelBlock), lds, s, e->p, nn_in, \
-                         leaf_o, max_descents, par, 0);                                    \
+                         leaf_o, max_descents, par, 0, nullptr, nullptr);                  \
   } while (0)
   if (e->p.K == 1)
     AZ_SEL_GO(1);
@@ -2227,6 +2268,21 @@ int az_select_move(az_engine* e, float* nn_in, int32_t* leaf_o, int32_t par, voi
   return launch_select(e, nn_in, leaf_o, par, move_blocks_for(e), azc::as_stream(stream));
 }
 
+int az_select_move_expand(az_engine* e, float* nn_in, int32_t* leaf_o, const float* priors,
+                          const float* values, int32_t par, void* stream) {
+  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select_move_expand: null argument");
+  AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_select_move_expand: deferred moves are off");
+  AZ_REQUIRE(par == 0 || par == 1, AZ_ERR_ARG, "az_select_move_expand: par must be 0 or 1");
+  AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
+             "az_select_move_expand: priors/values required in external-eval mode");
+  if (!priors || !values) {  // rollout mode: the expansion loads rows unconditionally
+    priors = e->d_zero_eval;
+    values = e->d_zero_eval + (size_t)e->p.G * e->p.K * 65;
+  }
+  return launch_select(e, nn_in, leaf_o, par, move_blocks_for(e), azc::as_stream(stream),
+                       priors, values, true);
+}
+
 int az_move_flush(az_engine* e, int32_t par, void* stream) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_move_flush: deferred moves are off");
@@ -2239,16 +2295,16 @@ int az_move_flush(az_engine* e, int32_t par, void* stream) {
   const int q = par ^ 1;
   if (e->p.K == 1)
     hipLaunchKernelGGL((k_select<1, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
-                       nullptr, 0, q, mb);
+                       nullptr, 0, q, mb, nullptr, nullptr);
   else if (e->p.K <= 2)
     hipLaunchKernelGGL((k_select<2, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
-                       nullptr, 0, q, mb);
+                       nullptr, 0, q, mb, nullptr, nullptr);
   else if (e->p.K <= 4)
     hipLaunchKernelGGL((k_select<4, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
-                       nullptr, 0, q, mb);
+                       nullptr, 0, q, mb, nullptr, nullptr);
   else
     hipLaunchKernelGGL((k_select<kMaxLeaves, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p,
-                       nullptr, nullptr, 0, q, mb);
+                       nullptr, nullptr, 0, q, mb, nullptr, nullptr);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -124,6 +124,15 @@ class Engine:
         nat.check(nat.lib.az_expand_backup_par(self.h, nat.ptr(pr), nat.ptr(va), int(par),
                                                self._s()), "az_expand_backup_par")
 
+    def select_move_expand(self, par, priors=None, values=None):
+        """One launch per step (az_select_move_expand): the previous step's leaves expanded
+        from priors / values, then this step's descents (+ the moves of the step before)."""
+        pr = self.priors if priors is None else priors
+        va = self.values if values is None else values
+        nat.check(nat.lib.az_select_move_expand(self.h, nat.ptr(self.nn_in), nat.ptr(self.leaf),
+                                                nat.ptr(pr), nat.ptr(va), int(par), self._s()),
+                  "az_select_move_expand")
+
     def move_flush(self, par):
         nat.check(nat.lib.az_move_flush(self.h, int(par), self._s()), "az_move_flush")
 
@@ -297,7 +306,7 @@ class BatchedSelfPlay:
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
                  device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1,
-                 require_graph=False, defer_moves=True, engine_stem=None):
+                 require_graph=False, defer_moves=True, engine_stem=None, fuse_expand=None):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -325,6 +334,12 @@ class BatchedSelfPlay:
         if self.defer_moves:
             self.engine.defer_moves(True)
         self._par = 0  # parity of the next step (deferred moves)
+        # fuse_expand (deferred moves only): the expansion of step n's leaves runs at the start
+        # of step n+1's select launch, by each slot's own wave -- one launch per step; default
+        # on, AZ_FUSE_EXPAND=0 turns it off (separate k_expand after the evaluation)
+        if fuse_expand is None:
+            fuse_expand = os.environ.get("AZ_FUSE_EXPAND", "1") != "0"
+        self.fuse_expand = bool(fuse_expand) and self.defer_moves
         # engine_stem: the net's stem runs in the select launch, by the wave that packs each
         # row (bit-identical; one launch and the planes' round trip fewer per step); default
         # on where the net supports it, AZ_ENGINE_STEM=0 turns it off
@@ -346,7 +361,9 @@ class BatchedSelfPlay:
 
     def _step_body(self, par=0):
         e = self.engine
-        if self.defer_moves:
+        if self.fuse_expand:
+            e.select_move_expand(par)  # the previous step's leaves, descents, its moves
+        elif self.defer_moves:
             e.select_move(par)  # + the previous step's moves
         else:
             e.select()
@@ -359,7 +376,9 @@ class BatchedSelfPlay:
                 pr, va = self.net.evaluate_planes(e.nn_in)
                 e.priors.copy_(pr)
                 e.values.copy_(va)
-        if self.defer_moves:
+        if self.fuse_expand:
+            pass  # expanded by the next step's launch (or step()'s flush)
+        elif self.defer_moves:
             e.expand_par(par)
         else:
             e.expand()
@@ -427,7 +446,10 @@ class BatchedSelfPlay:
                     if self.defer_moves:
                         self._par ^= 1
         if self.defer_moves and n > 0:
-            # the last step's moves, so results read after step() returns are complete
+            # the last step's leaves (fused expansion) and moves, so results read after step()
+            # returns are complete
+            if self.fuse_expand:
+                self.engine.expand_par(self._par ^ 1)
             self.engine.move_flush(self._par ^ 1)
 
     def play_games(self, n_games, max_steps=None, check_every=256):

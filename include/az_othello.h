@@ -216,6 +216,17 @@ int az_expand_backup_par(az_engine* eng, const float* priors, const float* value
                          void* stream);
 int az_move_flush(az_engine* eng, int32_t par, void* stream);
 
+/* Deferred moves with the expansion fused too (round 3): a step is ONE launch,
+ * az_select_move_expand(par) -> evaluation into priors / values, no az_expand_backup_par:
+ * each slot's wave first expands and backs up the previous step's waiting leaves from
+ * priors / values (the evaluation of that step), then descends; a search those leaves
+ * complete is moved by the next launch (the slot sits one step out).  Same games, samples
+ * and draws per slot as the plain order.  Before results are read:
+ * az_expand_backup_par(par) then az_move_flush(par) for the last step's parity par.
+ * Reference MCTS_model.py:325-360 (expand / evaluate / backup) with :372-395 (simulate). */
+int az_select_move_expand(az_engine* eng, float* nn_in, int32_t* leaf_o, const float* priors,
+                          const float* values, int32_t par, void* stream);
+
 /* AZ_RNG_INJECTED: per-slot streams, noise double [G, inj_noise_slots, 65] (Dirichlet
  * vectors, consumed at each root expansion with epsilon > 0) and uniforms double
  * [G, inj_uniform_slots] (consumed by the temperature-0 tie break and the action sample,

@@ -1,5 +1,6 @@
 """Deferred moves (az_engine_defer_moves / az_select_move / az_expand_backup_par /
-az_move_flush, BatchedSelfPlay's default): each step's move phase runs inside the next
+az_move_flush, and with the expansion fused too az_select_move_expand -- BatchedSelfPlay's
+default): each step's move phase runs inside the next
 step's select launch, beside its descents, instead of after expand.  A slot's games depend only on its own tree, policy and RNG stream -- never on
 the step its moves land in -- so every slot must produce exactly the games (training rows)
 of the plain move phase (az_play), bit for bit: reference self_play_worker.py:38-88 per
@@ -36,12 +37,14 @@ class MockNet(torch.nn.Module):
         return (h / 1024.0).float().contiguous(), ((k - 1000.0) / 1024.0).float().contiguous()
 
 
-def _run(defer, G, sims, steps, use_graph, leaves=1):
+def _run(defer, G, sims, steps, use_graph, leaves=1, fuse=True):
     args = {"c_puct": 2.0, "num_simulations": sims, "dirichlet_alpha": 1.0,
             "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
             "lambda": 0.98}
     sp = BatchedSelfPlay(MockNet(), args, G, seed=5, fold=False, use_graph=use_graph,
-                         defer_moves=defer, sample_capacity=G * 400, leaves_per_step=leaves)
+                         defer_moves=defer, sample_capacity=G * 400, leaves_per_step=leaves,
+                         fuse_expand=fuse)
+    assert sp.fuse_expand == (fuse and defer)
     sp.reset(start_budget=-1, stagger_steps=sims * 7)
     sp.step(steps)
     assert (sp.graph is not None) == use_graph and sp.graph_error is None
@@ -52,12 +55,16 @@ def _run(defer, G, sims, steps, use_graph, leaves=1):
     return c, {k: v[order] for k, v in s.items()}
 
 
-@pytest.mark.parametrize("use_graph,leaves", [(True, 1), (False, 1), (True, 4)])
-def test_deferred_moves_play_the_same_games(use_graph, leaves):
+@pytest.mark.parametrize("use_graph,leaves,fuse", [(True, 1, True), (False, 1, True),
+                                                   (True, 4, True), (True, 1, False),
+                                                   (True, 4, False)])
+def test_deferred_moves_play_the_same_games(use_graph, leaves, fuse):
+    """fuse: the expansion fused into the next step's select launch too
+    (az_select_move_expand, BatchedSelfPlay's default)."""
     G, sims = 512, 12
     steps = 2600 if leaves == 1 else 900
     c0, a = _run(False, G, sims, steps, use_graph, leaves)
-    c1, b = _run(True, G, sims, steps, use_graph, leaves)
+    c1, b = _run(True, G, sims, steps, use_graph, leaves, fuse)
     assert c0["games_finished"] >= G and c1["games_finished"] >= G
     compared = 0
     for g in range(G):
