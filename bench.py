@@ -142,19 +142,75 @@ def make_net(kind):
     return AlphaZeroNet(8, 65, 5, 128) if kind == "az5x128" else FastOthelloNet(8, 65)
 
 
-def launch_ms(launch, reps):
+class _HipEvents:
+    """HIP events created with hipEventDisableSystemFence (HIP's timing mode: recording the
+    event performs no system-scope cache writeback / invalidate inside the timed interval,
+    which a default event -- torch.cuda.Event -- does: "can improve the accuracy of timing
+    measurements", hip_runtime_api.h).  Through the HIP runtime torch already loaded (the
+    same libamdhip64.so soname, so the same runtime and streams)."""
+    FLAG_DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self):
+        import ctypes
+
+        self.ct = ctypes
+        self.lib = ctypes.CDLL("libamdhip64.so")
+        self.lib.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        self.lib.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                                 ctypes.c_void_p]
+        self.lib.hipEventDestroy.argtypes = [ctypes.c_void_p]
+
+    def create(self):
+        ev = self.ct.c_void_p()
+        assert self.lib.hipEventCreateWithFlags(self.ct.byref(ev), self.FLAG_DISABLE_SYSTEM_FENCE) == 0
+        return ev
+
+    def record(self, ev):
+        assert self.lib.hipEventRecord(ev, self.ct.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+
+    def elapsed_ms(self, e0, e1):
+        ms = self.ct.c_float()
+        assert self.lib.hipEventElapsedTime(self.ct.byref(ms), e0, e1) == 0
+        return ms.value
+
+    def destroy(self, ev):
+        self.lib.hipEventDestroy(ev)
+
+
+def launch_ms(launch, reps, system_fence=False, before=None):
     """Average duration of one launch: a HIP event pair around each launch on its stream
     (the current torch stream, which the entry points are given), so the figure is the
     kernel's own duration -- the quantity rocprofv3 --kernel-trace reports -- and not the
-    back-to-back loop's inter-launch gaps."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(reps)]
+    back-to-back loop's inter-launch gaps.  Events without the system-scope fence
+    (_HipEvents) by default; system_fence=True: torch's default events (each record
+    writes back and invalidates the caches inside the interval -- reported beside the
+    figure).  before(): untimed work ahead of each pair (e.g. restoring consumed inputs)."""
+    if system_fence:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(reps)]
+        for e0, e1 in evs:
+            if before:
+                before()
+            e0.record()
+            launch()
+            e1.record()
+        torch.cuda.synchronize()
+        return sum(e0.elapsed_time(e1) for e0, e1 in evs) / reps
+    he = _HipEvents()
+    evs = [(he.create(), he.create()) for _ in range(reps)]
     for e0, e1 in evs:
-        e0.record()
+        if before:
+            before()
+        he.record(e0)
         launch()
-        e1.record()
+        he.record(e1)
     torch.cuda.synchronize()
-    return sum(e0.elapsed_time(e1) for e0, e1 in evs) / reps
+    ms = sum(he.elapsed_ms(e0, e1) for e0, e1 in evs) / reps
+    for e0, e1 in evs:
+        he.destroy(e0)
+        he.destroy(e1)
+    return ms
 
 
 def playout_positions(games=4096, plies=60, seed=0xC0FFEE):
@@ -202,7 +258,7 @@ class StepKernelBench:
         self.args = [nat.ptr(x) for x in self.inp] + [nat.ptr(x) for x in self.outs] + \
             [nat.ptr(self.st), n, nat.stream_ptr()]
 
-    def time_ms(self, warm=400, reps=100):
+    def time_ms(self, warm=400, reps=100, system_fence=False):
         """Average launch time at steady state: `warm` untimed back-to-back launches first
         (the chip's power management takes ~8-200 launches of sustained load to settle
         from a cold start, during which launches run up to 40 % slower:
@@ -211,7 +267,7 @@ class StepKernelBench:
         for _ in range(warm):
             nat.check(nat.lib.oth_step_gpu(*self.args), "oth_step_gpu")
         torch.cuda.synchronize()
-        ms = launch_ms(lambda: nat.lib.oth_step_gpu(*self.args), reps)
+        ms = launch_ms(lambda: nat.lib.oth_step_gpu(*self.args), reps, system_fence)
         # spot-check the timed outputs against the host build of the same entry point
         own, opp, act = self.host
         k = min(self.n, len(own))
@@ -280,15 +336,7 @@ def conv_roofline(sp, device, n_boards):
         refill()
         nat.check(fn(*args), kname)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(100)]
-    for e0, e1 in evs:
-        refill()  # outside the timed pair
-        e0.record()
-        fn(*args)
-        e1.record()
-    torch.cuda.synchronize()
-    ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
+    ms = launch_ms(lambda: fn(*args), 100, before=refill)  # refill outside the timed pair
     flop = 2.0 * n_boards * 64 * C * C * 9
     achieved = mult * flop / (ms * 1e-3) / 1e12
     traffic = None  # HBM bytes per launch, PMC (scripts/pmc_conv.sh), for the default form
@@ -598,6 +646,7 @@ def main():
     if rank == 0 and not a.skip_kernel:
         kb = StepKernelBench(a.kernel_n, device)
         ms_step_kernel = kb.time_ms()
+        ms_step_fenced = kb.time_ms(warm=100, system_fence=True)
     sp.step(warmup_run)
     barrier()
     c0 = e.counters()
@@ -687,6 +736,11 @@ def main():
                               "gsteps_per_s": round(n / (ms * 1e-3) / 1e9, 2),
                               "inputs": "seeded random playouts (SURVEY.md 8d: seed 0xC0FFEE, "
                                         "plies 0-59, one legal action each), tiled to 2^24",
+                              "timing": "HIP event pair per launch on its stream, events "
+                                        "without the system-scope fence (hipEventDisableSystemFence)",
+                              "avg_launch_ms_default_events": round(ms_step_fenced, 4),
+                              "frac_default_events": round(STEP_BYTES * n / (ms_step_fenced * 1e-3)
+                                                           / 1e9 / HBM_PEAK_GBS, 4),
                               "avg_launch_ms_after_selfplay": round(ms_hot, 4),
                               "frac_after_selfplay": round(STEP_BYTES * n / (ms_hot * 1e-3)
                                                            / 1e9 / HBM_PEAK_GBS, 4)}
