@@ -218,16 +218,34 @@ class _EngineSearch:
 
     def _device_iteration(self):
         e = self.engine
+        if self.fuse_expand:
+            e.select_expand()  # the previous iteration's leaves, then this one's descents
+            self._evaluate()
+            return
         e.select()
         self._evaluate()
         e.expand()
 
     # False: the same n iterations run eagerly (tests/test_callers_gpu.py compares the two)
     use_graph = True
+    # True: each iteration is az_select_expand -> net (the expansion runs in the next
+    # iteration's select launch, one launch fewer per iteration; az_expand_backup after the
+    # last).  Off by default: one game's search is a latency chain, and the merged launch
+    # (the expansion's registers) measured no faster -- one_self_play 1.04-1.05 vs 1.07
+    # games/s unfused, same box (profiles/r03_dropin_fuse_expand_ab.json); AZ_DROPIN_FUSE=1
+    fuse_expand = os.environ.get("AZ_DROPIN_FUSE", "0") == "1"
 
     def _run_on_device(self, n):
         """n select -> net -> expand iterations with no host synchronisation, replayed from
         one captured HIP graph of a single iteration (captured on first use)."""
+        import torch
+
+        self._run_iterations(n)
+        if self.fuse_expand and n > 0:
+            with torch.no_grad():
+                self.engine.expand()  # the last iteration's leaves
+
+    def _run_iterations(self, n):
         import torch
 
         if not self.use_graph:

@@ -95,6 +95,7 @@ SIGNATURES = {
     "az_engine_set_stem": [_P, _P, _P, _P, _P, _I32],
     "az_select_move": [_P, _P, _P, _I32, _P],
     "az_select_move_expand": [_P, _P, _P, _P, _P, _I32, _P],
+    "az_select_expand": [_P, _P, _P, _P, _P, _P],
     "az_expand_backup_par": [_P, _P, _P, _I32, _P],
     "az_move_flush": [_P, _I32, _P],
     "az_inject": [_P, _P, _P, _P],

@@ -2283,6 +2283,19 @@ int az_select_move_expand(az_engine* e, float* nn_in, int32_t* leaf_o, const flo
                        priors, values, true);
 }
 
+int az_select_expand(az_engine* e, float* nn_in, int32_t* leaf_o, const float* priors,
+                     const float* values, void* stream) {
+  AZ_REQUIRE(e && nn_in, AZ_ERR_ARG, "az_select_expand: null argument");
+  AZ_REQUIRE(!e->p.defer, AZ_ERR_STATE, "az_select_expand: deferred moves are on (az_select_move_expand)");
+  AZ_REQUIRE(e->p.eval_mode == AZ_EVAL_ROLLOUT || (priors && values), AZ_ERR_ARG,
+             "az_select_expand: priors/values required in external-eval mode");
+  if (!priors || !values) {  // rollout mode: the expansion loads rows unconditionally
+    priors = e->d_zero_eval;
+    values = e->d_zero_eval + (size_t)e->p.G * e->p.K * 65;
+  }
+  return launch_select(e, nn_in, leaf_o, 0, 0, azc::as_stream(stream), priors, values, true);
+}
+
 int az_move_flush(az_engine* e, int32_t par, void* stream) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   AZ_REQUIRE(e->p.defer, AZ_ERR_STATE, "az_move_flush: deferred moves are off");

@@ -133,6 +133,15 @@ class Engine:
                                                 nat.ptr(pr), nat.ptr(va), int(par), self._s()),
                   "az_select_move_expand")
 
+    def select_expand(self, priors=None, values=None):
+        """az_select_expand: the previous select's leaves expanded from priors / values, then
+        this select's descents, one launch (engines without deferred moves)."""
+        pr = self.priors if priors is None else priors
+        va = self.values if values is None else values
+        nat.check(nat.lib.az_select_expand(self.h, nat.ptr(self.nn_in), nat.ptr(self.leaf),
+                                           nat.ptr(pr), nat.ptr(va), self._s()),
+                  "az_select_expand")
+
     def move_flush(self, par):
         nat.check(nat.lib.az_move_flush(self.h, int(par), self._s()), "az_move_flush")
 

@@ -227,6 +227,14 @@ int az_move_flush(az_engine* eng, int32_t par, void* stream);
 int az_select_move_expand(az_engine* eng, float* nn_in, int32_t* leaf_o, const float* priors,
                           const float* values, int32_t par, void* stream);
 
+/* The same fusion for engines without deferred moves (the drop-in MCTS's host-driven
+ * search): az_select_expand = the expansion of the previous az_select's leaves from priors /
+ * values, then az_select's descents, in one launch; a search the expansion completes is
+ * marked done and the launch emits no leaf for it.  az_expand_backup after the last one.
+ * Reference MCTS_model.py:325-360 with :372-395. */
+int az_select_expand(az_engine* eng, float* nn_in, int32_t* leaf_o, const float* priors,
+                     const float* values, void* stream);
+
 /* AZ_RNG_INJECTED: per-slot streams, noise double [G, inj_noise_slots, 65] (Dirichlet
  * vectors, consumed at each root expansion with epsilon > 0) and uniforms double
  * [G, inj_uniform_slots] (consumed by the temperature-0 tie break and the action sample,

@@ -96,8 +96,9 @@ def test_dropin_net_search_graph_replay_equals_eager(threads, monkeypatch):
     from MCTS_model import _EngineSearch
     from Models import AlphaZeroNet
 
-    def run(use_graph):
+    def run(use_graph, fuse=True):
         monkeypatch.setattr(_EngineSearch, "use_graph", use_graph)
+        monkeypatch.setattr(_EngineSearch, "fuse_expand", fuse)
         torch.manual_seed(0)
         net = AlphaZeroNet(8, 65, 5, 128)
         env = OthelloGameNew(8)
@@ -118,8 +119,11 @@ def test_dropin_net_search_graph_replay_equals_eager(threads, monkeypatch):
         assert (getattr(mcts._impl, "_graph", None) is not None) == use_graph
         return out
 
-    g, e = run(True), run(False)
-    for ply, (a, b) in enumerate(zip(g, e)):
-        assert np.array_equal(a[0], b[0]), ply
-        assert a[1] == b[1] and a[2] == b[2], ply
-        assert np.array_equal(a[3], b[3]), ply
+    # fused (az_select_expand: each iteration's expansion in the next select launch, the
+    # default) and unfused iterations, replayed and eager: the same searches
+    e = run(False, False)
+    for other in (run(True, True), run(False, True), run(True, False)):
+        for ply, (a, b) in enumerate(zip(other, e)):
+            assert np.array_equal(a[0], b[0]), ply
+            assert a[1] == b[1] and a[2] == b[2], ply
+            assert np.array_equal(a[3], b[3]), ply
