@@ -79,6 +79,12 @@
 #ifndef AZ_W4_PRIO
 #define AZ_W4_PRIO 0
 #endif
+// streaming cache hint (experiments): bit 0 = the input loads and the residual LDS-DMA
+// non-temporal (nt), bit 1 = the output stores non-temporal -- so the activations stream
+// past L2 instead of evicting the weight set every workgroup re-reads from it
+#ifndef AZ_W4_NT
+#define AZ_W4_NT 0
+#endif
 // timing proxy of a two-plane split (wrong numerics): 2 planes, 3 products
 #ifndef AZ_W4_PROXY2
 #define AZ_W4_PROXY2 0
@@ -319,7 +325,8 @@ __device__ __forceinline__ void load_in(f32x4 (&ld)[G::LD_PER_THREAD], __amdgpu_
   const int c = L & 7;
 #pragma unroll
   for (int j = 0; j < G::LD_PER_THREAD; ++j)
-    ld[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, goff[j], c * 64, 0));
+    ld[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, goff[j], c * 64,
+                                                                             (AZ_W4_NT & 1) ? 2 : 0));
 }
 
 // ... and into the slot's padded interior
@@ -555,10 +562,16 @@ __device__ __forceinline__ int qmap(const St<G>& S, int vq) {
 // byte address lds_dst + 16 i.  Issued as asm so the compiler's vmcnt bookkeeping for the
 // weight and input loads is not collapsed to vmcnt(0) around it; its completion is waited
 // for explicitly (vmcnt(0)) before the barrier that precedes the reads
+#if AZ_W4_NT & 1
+#define AZ_W4_DMA_CPOL " nt"
+#else
+#define AZ_W4_DMA_CPOL ""
+#endif
 __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" AZ_W4_DMA_CPOL
+      "\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_dst));
 }
@@ -784,7 +797,10 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
         if constexpr (HEADS) {  // kept for the fused heads (heads_epilogue), not stored
           S.Y[I][j][t][e] = v;
         } else {
-          y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
+          if constexpr ((AZ_W4_NT & 2) != 0)
+            __builtin_nontemporal_store(v, &y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co]);
+          else
+            y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
           E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fabsf(v));
         }
       }

@@ -1,5 +1,7 @@
 """Run one trunk-conv kernel `reps` times (for rocprofv3 counter passes):
-    python scripts/conv_one.py az_conv3x3_wino4_gpu split3 1024 20"""
+    python scripts/conv_one.py az_conv3x3_wino4_gpu split3 1024 20 [calib]
+With `calib`, a torch copy_ of 2 x 256 MiB follows (the HBM-counter calibration of
+scripts/step_kernel_bench.py: 268,435,456 bytes read + written)."""
 import os
 import sys
 
@@ -41,6 +43,10 @@ def main():
         if work is not None:
             work.copy_(amax)  # the kernel consumes (zeroes) its in_absmax
         nat.check(fn(*args, nat.stream_ptr()), name)
+    if len(sys.argv) > 5 and sys.argv[5] == "calib":
+        a = torch.empty(64 << 20, dtype=torch.float32, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a)
     torch.cuda.synchronize()
     print("ok", name, mode_name, B, reps)
 
