@@ -73,6 +73,19 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 #define AZ_STEP_GRID_CAP (256 * 64)
 #endif
 
+// non-temporal output stores (1, the product); 0 = plain stores (A/B builds)
+#ifndef AZ_STEP_NT_ST
+#define AZ_STEP_NT_ST 1
+#endif
+
+template <class T>
+__device__ __forceinline__ void st_out(T v, T* p) {
+  if constexpr (AZ_STEP_NT_ST)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 // one lane's pair of inputs (a = own, b = opp, c = the two actions)
 struct PairIn {
   u64x2 a, b;
@@ -129,11 +142,10 @@ __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ o
     char* lo = reinterpret_cast<char*>(legal_o) + o16;
     if (live1) {
       const u64x2 vo = {o0, o1}, vp = {p0, p1}, vl = {l0, l1};
-      __builtin_nontemporal_store(vo, reinterpret_cast<u64x2*>(oo));
-      __builtin_nontemporal_store(vp, reinterpret_cast<u64x2*>(po));
-      __builtin_nontemporal_store(vl, reinterpret_cast<u64x2*>(lo));
-      __builtin_nontemporal_store((uint32_t)s0 | ((uint32_t)s1 << 16),
-                                  reinterpret_cast<uint32_t*>(status_o) + j);
+      st_out(vo, reinterpret_cast<u64x2*>(oo));
+      st_out(vp, reinterpret_cast<u64x2*>(po));
+      st_out(vl, reinterpret_cast<u64x2*>(lo));
+      st_out((uint32_t)s0 | ((uint32_t)s1 << 16), reinterpret_cast<uint32_t*>(status_o) + j);
     } else if (live0) {
       *reinterpret_cast<uint64_t*>(oo) = o0;
       *reinterpret_cast<uint64_t*>(po) = p0;
