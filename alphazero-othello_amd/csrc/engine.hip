@@ -44,6 +44,16 @@ constexpr int kMoveBlock = 256;
 constexpr int kMaxPath = 64;     // one wave lane per path depth for the parallel backup
 constexpr int kMaxLeaves = 8;    // leaves_per_step limit (virtual-loss descents per step)
 
+// One leaf per slot and step (K = 1): a select wave starts another descent (after terminal
+// ones, backed up in place) only while this launch's descents walked fewer than this many
+// tree levels, beside the max_descents cap -- the launch's span is its deepest end-game
+// slot's chain of descents (~1.4 us per level at full load).  With one leaf per step a
+// slot's sequence of descents and backups does not depend on where the launches split it,
+// so games are unchanged; K > 1 keeps the cap alone (its virtual-loss batches would
+// change).  14 measured best of 10 / 14 / 18 (profiles/r03_sel_levels_ab.json); 0 = off.
+#ifndef AZ_SEL_LEVELS
+#define AZ_SEL_LEVELS 14
+#endif
 #ifndef AZ_ENG_STAMP
 #define AZ_ENG_STAMP 0
 #endif
@@ -653,6 +663,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
     // the expansion's and backup's stores before this wave's descent loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
+  ENG_STAMP(2);
   const int status = p.g.status[g];
   // the stagger schedule counts steps: the engine's, or the slot's own with deferred moves
   // (the engine's counter is advanced inside a deferred launch)
@@ -714,7 +725,9 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
     wait_leaf();  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
   } else {
     int guard = 0;
-    while (sims_done + w.n < target && w.n < K && guard < max_descents) {
+    int levels = 0;  // tree levels walked by this launch's descents (AZ_SEL_LEVELS, K = 1)
+    while (sims_done + w.n < target && w.n < K && guard < max_descents &&
+           (KMAX > 1 || AZ_SEL_LEVELS == 0 || levels < AZ_SEL_LEVELS)) {
       if (guard > 0) cur = load_root(p, g, half, kid0);  // the last backup changed the root's N
       ++guard;
       depth = 0;
@@ -745,8 +758,13 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
         ++depth;
         if (lane == depth) path_node = cur.node;
       }
+      levels += depth + 1;
     }
   }
+  ENG_STAMP(6);
+#if AZ_ENG_STAMP
+  st_[7] = (unsigned long long)depth;
+#endif
   for (int j = w.n; j < K; ++j) {
     emit_none(nn_in, leaf_o, row0 + j);
     if (KMAX > 1 && lane == 0) p.g.leaf[row0 + j] = -1;

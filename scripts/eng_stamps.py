@@ -79,6 +79,44 @@ def main():
         out[name]["launch_median_wave_end_offset"] = stats(ends)
         if kind == 3:
             out[name]["wave_total"] = stats(r[:, 3] - r[:, 1])
+    # the merged select launch (deferred moves + fused expansion): per launch, when each
+    # select wave's phases end relative to the launch's first start (expansion -> [2],
+    # descent -> [6], stem / bookkeeping -> [3]; [7] = the last descent's depth) and when the
+    # move workgroups (kind 1, ends at [7]) end
+    r = a[(a[:, 0] == 3) | (a[:, 0] == 1)]
+    r = r[np.argsort(r[:, 1])]
+    if len(r):
+        cut = np.flatnonzero(np.diff(r[:, 1]) > 10000) + 1
+        lw = {"span": [], "slowest_select_start": [], "slowest_select_expand": [],
+              "slowest_select_descent": [], "slowest_select_finish": [], "slowest_select_depth": [],
+              "slowest_is_move": [], "move_end_max": [], "select_end_p50": [], "select_end_p99": []}
+        ph = {"expand": [], "descent": [], "finish": [], "depth": []}
+        for grp in np.split(r, cut):
+            sel, mvg = grp[grp[:, 0] == 3], grp[grp[:, 0] == 1]
+            if len(sel) < 256:
+                continue
+            t0 = grp[:, 1].min()
+            send = sel[:, 3] - t0
+            mend = (mvg[:, 7] - t0) if len(mvg) else np.zeros(1, np.int64)
+            lw["span"].append(max(send.max(), mend.max()))
+            lw["move_end_max"].append(mend.max())
+            lw["select_end_p50"].append(np.percentile(send, 50))
+            lw["select_end_p99"].append(np.percentile(send, 99))
+            lw["slowest_is_move"].append(100 * int(mend.max() > send.max()))
+            w = sel[np.argmax(send)]
+            lw["slowest_select_start"].append(w[1] - t0)
+            lw["slowest_select_expand"].append(w[2] - w[1])
+            lw["slowest_select_descent"].append(w[6] - w[2])
+            lw["slowest_select_finish"].append(w[3] - w[6])
+            lw["slowest_select_depth"].append(100 * w[7])
+            ph["expand"] += list(sel[:, 2] - sel[:, 1])
+            ph["descent"] += list(sel[:, 6] - sel[:, 2])
+            ph["finish"] += list(sel[:, 3] - sel[:, 6])
+            ph["depth"] += list(100 * sel[:, 7])
+        out["merged_select_per_launch"] = {k: stats(v) for k, v in lw.items()}
+        out["merged_select_wave_phases"] = {k: stats(v) for k, v in ph.items()}
+        out["merged_select_note"] = ("us; *_depth and slowest_is_move are x100 "
+                                     "(depth in levels, is_move as a percentage)")
     # the slowest k_expand waves: leaf (0 = a root expansion), path length, arena size, slot
     ex = ex[np.argsort(ex[:, 3] - ex[:, 1])]
     out["k_expand_slowest"] = [{"us": round((r[3] - r[1]) / 100.0, 2), "leaf": int(r[4]),
