@@ -672,6 +672,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
   const int half = p.g.half[g];
   int sims_done = p.g.sims_done[g];
   const int target = p.g.sims_target[g];
+  // the slot's counters as of this point (only this wave writes them from here on): the end
+  // of the launch updates them without another load round trip
+  const int sims0 = sims_done;
+  const unsigned long long acc0 = p.g.sims_acc[g];
   if (status != kActive || (long long)step < (long long)start_step) {
     emit_none_rows(p, nn_in, leaf_o, row0, K);
     return;
@@ -775,9 +779,8 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p, float* __restric
       if (j < K) emit_stem(p, row0 + j, plane[j]);
   }
   if (lane == 0) {
-    const int prev = p.g.sims_done[g];
-    if (sims_done != prev) {
-      p.g.sims_acc[g] += (unsigned long long)(sims_done - prev);
+    if (sims_done != sims0) {
+      p.g.sims_acc[g] = acc0 + (unsigned long long)(sims_done - sims0);
       p.g.sims_done[g] = sims_done;
     }
     if (w.n == 0 && sims_done >= target) {
