@@ -325,6 +325,9 @@ __device__ void backup_path(const Params& p, int g, int half, int path_node, int
 #ifndef AZ_STEM_NOSTORE
 #define AZ_STEM_NOSTORE 0
 #endif
+#ifndef AZ_STEM_PK
+#define AZ_STEM_PK 1  // 128 channels: the two channels of a lane as packed fp32 fma
+#endif
 #ifndef AZ_STEM_CODE
 #define AZ_STEM_CODE 1  // experiment builds: 0 compiles the engine stem out
 #endif
@@ -348,8 +351,18 @@ __device__ __forceinline__ void stem_board_row(const VecT (&w)[9], VecT b, float
       const int dy = t / 3 - 1, xx = px + t % 3 - 1;
       if (dy < DYLO || dy > DYHI || xx < 0 || xx > 7) continue;
       if constexpr (V == 2) {
+#if AZ_STEM_PK
+        // both channels in one v_pk_fma_f32 (per component the same single-rounding fma)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v s2 = {v[dy + 1][xx], v[dy + 1][xx]}, w2 = {w[t].x, w[t].y};
+        f2v a2 = {acc.x, acc.y};
+        a2 = __builtin_elementwise_fma(s2, w2, a2);
+        acc.x = a2.x;
+        acc.y = a2.y;
+#else
         acc.x = fmaf(v[dy + 1][xx], w[t].x, acc.x);
         acc.y = fmaf(v[dy + 1][xx], w[t].y, acc.y);
+#endif
       } else {
         acc = fmaf(v[dy + 1][xx], w[t], acc);
       }
