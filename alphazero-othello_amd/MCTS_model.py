@@ -299,9 +299,12 @@ class _EngineSearch:
             leaf = int(e.leaf[0].item())
             if leaf < 0:
                 info = e.game_info()
-                if info["status"][0] != 1 or guard > 1000:
+                if info["status"][0] != 1:
                     break
                 guard += 1
+                if guard > 1000:
+                    raise RuntimeError("MCTS search made no progress in 1,000 selects "
+                                       "(engine descent budget exhausted)")
                 continue
             if self.policy is not None:
                 self._evaluate()

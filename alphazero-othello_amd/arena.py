@@ -23,14 +23,16 @@ INIT_OWN, INIT_OPP = 0x0000000810000000, 0x0000001008000000
 
 
 def _as_evaluator(net, device):
-    """nn.Module -> batched device evaluator over the engine's planes; callables pass
-    through (device-side test policies); None = rollout evaluation."""
+    """nn.Module -> its fused inference copy (evaluate_into straight into the engine's
+    buffers, graph-capturable); callables pass through (device-side test policies: eager
+    steps); None = rollout evaluation."""
     if net is None or callable(net) and not isinstance(net, torch.nn.Module):
+        return net
+    if hasattr(net, "evaluate_into"):  # already an inference form (FusedInferenceNet, ...)
         return net
     from Models import inference_copy
 
-    m = inference_copy(net, device)
-    return m.evaluate_planes
+    return inference_copy(net, device)
 
 
 def tie_break_random(best):
@@ -42,12 +44,23 @@ def tie_break_lowest(best):
 
 
 class BatchedArena:
+    """Two host-driven engines (one per net), slot g of each holding that net's tree of
+    match g.  A search is replayed from HIP graphs: ceil(sims / K) + 1 iterations of
+    select -> net -> expand complete every searching slot (a host-driven select waits on
+    min(K, remaining) leaves or finishes its search), with one status check after them.
+    Matches are laid out so that a net's searching slots are one contiguous half of the
+    wave (the matches where it plays first, then the others: with colours alternating, the
+    side to move at a ply is one colour in every match), and the net evaluates only that
+    half's rows."""
+
     def __init__(self, net_a, net_b, args, n_slots, device=None, seed=0,
-                 tie_break=tie_break_random, node_capacity=0):
+                 tie_break=tie_break_random, node_capacity=0, use_graph=True,
+                 steps_per_graph=8):
         self.args = args
         self.G = n_slots
+        self.K = min(8, max(1, int(args.get("num_threads", 4))))
         kw = dict(c_puct=args["c_puct"], auto_play=False, node_capacity=node_capacity,
-                  device=device, leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
+                  device=device, leaves_per_step=self.K)
         self.eng = [Engine(n_slots, args["num_simulations"], rollout=net_a is None, seed=seed,
                            **kw),
                     Engine(n_slots, args["num_simulations"], rollout=net_b is None,
@@ -55,27 +68,90 @@ class BatchedArena:
         dev = self.eng[0].device
         self.eval = [_as_evaluator(net_a, dev), _as_evaluator(net_b, dev)]
         self.tie_break = tie_break
+        # graphs need every evaluator on device buffers only (rollout or a fused inference
+        # copy); test callables run eagerly
+        self.use_graph = use_graph and all(ev is None or hasattr(ev, "evaluate_into")
+                                           for ev in self.eval)
+        self.steps_per_graph = max(1, int(steps_per_graph))
+        self._graphs = {}
+        self._bounds = (0, n_slots, n_slots)  # (0, end of the first-player half, n)
+        self.iterations = 0  # select -> net -> expand iterations run (per searching engine)
 
-    def _search(self, slots, check_every=8):
+    def _row_range(self, sel):
+        """The slot range whose rows a net evaluates: the half of the wave holding every
+        searching slot, else the whole wave."""
+        lo, mid, hi = self._bounds
+        if sel.min() >= lo and sel.max() < mid:
+            return (lo, mid)
+        if sel.min() >= mid and sel.max() < hi:
+            return (mid, hi)
+        return (lo, hi)
+
+    def _iteration(self, plan):
+        """One select -> net -> expand per (engine, slot range) of the plan."""
+        K = self.K
+        for k, (lo, hi) in plan:
+            e = self.eng[k]
+            e.select()
+            ev = self.eval[k]
+            r0, r1 = lo * K, hi * K
+            if ev is None:
+                pass  # rollout: the expansion evaluates on device
+            elif hasattr(ev, "evaluate_into"):
+                ev.evaluate_into(e.nn_in[r0:r1], e.priors[r0:r1], e.values[r0:r1])
+            else:
+                pr, va = ev(e.nn_in[r0:r1])
+                e.priors[r0:r1].copy_(pr)
+                e.values[r0:r1].copy_(va)
+            e.expand()
+
+    def _run(self, plan, n):
+        """n iterations of the plan: graphs of steps_per_graph iterations (and single ones
+        for the remainder), each captured on first use after one eager iteration."""
+        self.iterations += n
+        if not self.use_graph:
+            for _ in range(n):
+                self._iteration(plan)
+            return
+        while n > 0:
+            m = self.steps_per_graph if n >= self.steps_per_graph else 1
+            g = self._graphs.get((plan, m))
+            if g is None:
+                s = torch.cuda.Stream(device=self.eng[0].device)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    self._iteration(plan)  # warms the kernels and caches; real work
+                torch.cuda.current_stream().wait_stream(s)
+                n -= 1
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(m):
+                        self._iteration(plan)
+                self._graphs[(plan, m)] = g
+                continue
+            g.replay()
+            n -= m
+
+    @torch.no_grad()
+    def _search(self, slots):
         sims = self.args["num_simulations"]
-        live = []
+        plan = []
         for k in (0, 1):
             if len(slots[k]):
                 self.eng[k].begin_search_slots(slots[k], sims)
-                live.append(k)
-        with torch.no_grad():
-            while live:
-                for _ in range(check_every):
-                    for k in live:
-                        e = self.eng[k]
-                        e.select()
-                        if self.eval[k] is not None:
-                            pr, va = self.eval[k](e.nn_in)
-                            e.priors.copy_(pr)
-                            e.values.copy_(va)
-                        e.expand()
-                live = [k for k in live
-                        if (self.eng[k].game_info()["status"] == nat.AZ_GAME_ACTIVE).any()]
+                plan.append((k, self._row_range(slots[k])))
+        plan = tuple(plan)
+        # every searching slot finishes within ceil(sims / K) + 1 iterations (the root's
+        # expansion included); the loop confirms, and would finish a straggler step by step
+        self._run(plan, -(-sims // self.K) + 1)
+        for _ in range(1000):
+            plan = tuple((k, r) for k, r in plan
+                         if (self.eng[k].game_info()["status"] == nat.AZ_GAME_ACTIVE).any())
+            if not plan:
+                break
+            self._run(plan, 1)
+        else:
+            raise RuntimeError("arena search did not finish")
         for k in (0, 1):
             # a skipped expansion (node arena full, or a waiting descent deeper than the
             # tracked path) makes that search differ from the reference's: never score it
@@ -90,8 +166,16 @@ class BatchedArena:
         plies = []
         for base in range(0, n_matches, self.G):
             n = min(self.G, n_matches - base)
-            a_first = (np.arange(base, base + n) % 2) == 0
-            res, pl = self._play_wave(a_first)
+            # colours alternate by match index (eval.py:105-112: even -> A first); slot s of
+            # the wave holds match perm[s], the matches where A plays first in the first
+            # slots, so each net's searching slots at a ply are one half
+            a_first_m = (np.arange(base, base + n) % 2) == 0
+            perm = np.argsort(~a_first_m, kind="stable")
+            self._bounds = (0, int(a_first_m.sum()), n)
+            res, pl_s = self._play_wave(a_first_m[perm])
+            pl = np.empty(n, np.int64)
+            pl[perm] = pl_s  # plies in match order
+            pl = [int(x) for x in pl]
             wins_a += int((res == 1).sum())
             wins_b += int((res == -1).sum())
             draws += int((res == 0).sum())

@@ -132,24 +132,6 @@ __device__ unsigned long long g_w4_cst[256 * 8 * 32 * 3];
   do {                  \
   } while (0)
 #endif
-// experiment builds only (-DAZ_W4_CSTAMP=1): every wave's s_memtime at each chunk's start,
-// before and after its closing barrier, [wg < 256][wave][chunk][3], lane 0's vector store
-#ifndef AZ_W4_CSTAMP
-#define AZ_W4_CSTAMP 0
-#endif
-#if AZ_W4_CSTAMP
-__device__ unsigned long long g_w4_cst[256 * 8 * 32 * 3];
-#define W4C_STAMP(v, i)                                                                     \
-  do {                                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (v) < 32)                            \
-      g_w4_cst[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (v)) * 3 + (i)] = t_;          \
-  } while (0)
-#else
-#define W4C_STAMP(v, i) \
-  do {                  \
-  } while (0)
-#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -603,7 +585,6 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
-  W4C_STAMP(v, 0);
   W4C_STAMP(v, 0);
   const int L = lmap<G>(S, v);
   const char* cur = S.lds + (v & 1) * G::BUF;
@@ -1286,12 +1267,18 @@ int launch_wino4_splitk(const float* x, const void* wq, const float* bias, const
 
 }  // namespace
 
+// the buffer-descriptor streams address activations with 32-bit byte offsets (num_records
+// is at most 2^31 - 1): n_boards * 64 * 128 channels * 4 B must stay below that
+constexpr int32_t kW4MaxBoards = 0x7fffffff / (64 * 128 * 4);
+
 extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const float* bias,
                                            const float* res, float* y, int32_t n_boards,
                                            int32_t channels, int32_t relu, int32_t mode,
                                            float* in_absmax, float* out_absmax, float* part,
                                            int32_t splits, void* stream) {
-  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_splitk_gpu: n_boards < 0");
+  AZ_REQUIRE(n_boards >= 0 && n_boards <= kW4MaxBoards, AZ_ERR_ARG,
+             "az_conv3x3_wino4_splitk_gpu: n_boards %d outside [0, %d] (32-bit buffer offsets)", n_boards,
+             kW4MaxBoards);
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(x && wq && bias && y && part && in_absmax && x != y && (!res || res != y) &&
                  in_absmax != out_absmax,
@@ -1325,13 +1312,6 @@ extern "C" int az_w4_cstamps(unsigned long long* host, int n) {
 }
 #endif
 
-#if AZ_W4_CSTAMP
-extern "C" int az_w4_cstamps(unsigned long long* host, int n) {
-  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_cst), sizeof(unsigned long long) * n));
-  return AZ_OK;
-}
-#endif
-
 #if AZ_W4_STAMP
 extern "C" int az_w4_stamps(unsigned long long* host, int n) {
   AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_stamps), sizeof(unsigned long long) * n));
@@ -1347,7 +1327,9 @@ extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const 
                                           const float* w1T, const float* b1, const float* w2,
                                           const float* b2, float* priors, float* values,
                                           void* stream) {
-  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_heads_gpu: n_boards < 0");
+  AZ_REQUIRE(n_boards >= 0 && n_boards <= kW4MaxBoards, AZ_ERR_ARG,
+             "az_conv3x3_wino4_heads_gpu: n_boards %d outside [0, %d] (32-bit buffer offsets)", n_boards,
+             kW4MaxBoards);
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(x && wq && bias && res && in_absmax && wpv && bpv && wpolT && bpol && w1T && b1 &&
                  w2 && b2 && priors && values,
@@ -1384,7 +1366,9 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
                                   const float* stem_b, float* h_in, float* hb0, float* hb1,
                                   float* t, float* amax0, float* amax1, int32_t n_boards,
                                   int32_t n_convs, int32_t channels, void* stream) {
-  AZ_REQUIRE(n_boards >= 0 && n_convs >= 0, AZ_ERR_ARG, "az_trunk_wino4_gpu: negative size");
+  AZ_REQUIRE(n_boards >= 0 && n_convs >= 0 && n_boards <= kW4MaxBoards, AZ_ERR_ARG,
+             "az_trunk_wino4_gpu: n_boards %d / n_convs %d out of range (n_boards <= %d)",
+             n_boards, n_convs, kW4MaxBoards);
   if (n_boards == 0 || (n_convs == 0 && !planes)) return AZ_OK;
   AZ_REQUIRE((n_convs == 0 || (wq && bias)) && h_in && hb0 && hb1 && t && amax0 && amax1,
              AZ_ERR_ARG,
@@ -1418,7 +1402,9 @@ extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float*
                                     const float* res, float* y, int32_t n_boards,
                                     int32_t channels, int32_t relu, int32_t mode,
                                     float* in_absmax, float* out_absmax, void* stream) {
-  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_conv3x3_wino4_gpu: n_boards < 0");
+  AZ_REQUIRE(n_boards >= 0 && n_boards <= kW4MaxBoards, AZ_ERR_ARG,
+             "az_conv3x3_wino4_gpu: n_boards %d outside [0, %d] (32-bit buffer offsets)", n_boards,
+             kW4MaxBoards);
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(x && wq && bias && y && x != y && (!res || res != y), AZ_ERR_ARG,
              "az_conv3x3_wino4_gpu: null buffer or in-place call");

@@ -315,7 +315,8 @@ class BatchedSelfPlay:
     def __init__(self, net, args, n_games, seed=0, stream_id=0, d4_augment=False,
                  dtype=torch.float32, node_capacity=0, sample_capacity=0, use_graph=True,
                  device=None, fold=True, steps_per_graph=8, precision=None, leaves_per_step=1,
-                 require_graph=False, defer_moves=True, engine_stem=None, fuse_expand=None):
+                 require_graph=False, defer_moves=True, engine_stem=None, fuse_expand=None,
+                 injected_rng=False, inj_noise_slots=1, inj_uniform_slots=1):
         from Models import inference_copy
 
         self.args = dict(args)
@@ -328,7 +329,8 @@ class BatchedSelfPlay:
             lambd=args.get("lambda", 1.0), rollout=net is None, d4_augment=d4_augment,
             auto_play=True, refill=True, node_capacity=node_capacity,
             sample_capacity=sample_capacity, seed=seed, stream_id=stream_id, device=device,
-            leaves_per_step=leaves_per_step)
+            leaves_per_step=leaves_per_step, injected_rng=injected_rng,
+            inj_noise_slots=inj_noise_slots, inj_uniform_slots=inj_uniform_slots)
         self.device = self.engine.device
         if net is None:
             self.net = None
@@ -423,6 +425,13 @@ class BatchedSelfPlay:
 
     def reset(self, start_budget=-1, stagger_steps=0):
         self.engine.reset_all(start_budget, stagger_steps)
+
+    def inject(self, noise=None, uniforms=None):
+        """Injected-RNG engines (injected_rng=True): per-slot Dirichlet vectors
+        [G, inj_noise_slots, 65] and uniforms [G, inj_uniform_slots] (Engine.inject) replace the
+        device Philox draws, so recorded reference games replay through this exact path
+        (tests/test_bench_path_gpu.py).  A slot's cursors run on across its games."""
+        self.engine.inject(noise, uniforms)
 
     @torch.no_grad()
     def step(self, n=1):

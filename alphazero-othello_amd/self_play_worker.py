@@ -67,12 +67,58 @@ def one_self_play(args_tuple):
 
 
 def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, stream_id=0,
-                            d4_augment=False, dtype=torch.float32):
+                            d4_augment=False, dtype=torch.float32, group=None,
+                            sync_weights=True):
     """Batched replacement of Trainer.collect_self_play_games' pool (train.py:199-225):
-    `num_games` games on one GPU, `n_slots` at a time (default min(num_games, 4096)), each
+    `num_games` games on the GPU, `n_slots` at a time (default min(games, 4096)), each
     searching with args['num_threads'] virtual-loss leaves per step (the reference's worker
-    count, default 4: MCTS_model.py:196).  Returns the concatenated training tuples of all
-    games."""
+    count, default 4: MCTS_model.py:196).  Returns the training tuples of all games.
+
+    Under torch.distributed (one process per GPU, `group` or the default group, world > 1)
+    this is one generation of the whole node: rank r plays its share of
+    `num_games` (num_games // world, the first num_games % world ranks one more) on its own
+    Philox sub-stream (stream_id + r), with the best net's weights first broadcast from rank
+    0 (`sync_weights`; the reference hands every pool worker the best net's state_dict,
+    train.py:205-207), and ONE all-gather (dist_replay.allgather_samples: RCCL over xGMI
+    with the "nccl" backend) pools every rank's rows on every rank -- each rank returns the
+    same list, rank 0's games first."""
+    import torch.distributed as dist
+
+    distributed = dist.is_available() and dist.is_initialized() and \
+        dist.get_world_size(group) > 1
+    if not distributed:
+        rows = _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype)
+        return _rows_to_tuples(rows)
+    from dist_replay import allgather_samples, broadcast_state_dict
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = _collective_device(group)
+    if sync_weights and policy is not None:
+        home = next(iter(policy.parameters())).device
+        broadcast_state_dict(policy.to(dev), src=0, group=group)
+        policy.to(home)
+    mine = num_games // world + (1 if rank < num_games % world else 0)
+    rows = _local_rows(policy, args, mine, n_slots, seed, stream_id + rank, d4_augment, dtype)
+    pooled, _ = allgather_samples(rows, dev, group=group)
+    return _rows_to_tuples({k: v.cpu().numpy() for k, v in pooled.items()})
+
+
+def _collective_device(group=None):
+    """Tensors for the group's backend: the rank's GPU for RCCL ("nccl"), the host for gloo."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype):
+    """This process's games as engine sample rows (numpy: own/opp canonical bitboards, pi,
+    z, player); none when num_games is 0."""
+    if num_games <= 0:
+        return {"own": np.zeros(0, np.uint64), "opp": np.zeros(0, np.uint64),
+                "pi": np.zeros((0, 65), np.float32), "z": np.zeros(0, np.float64),
+                "player": np.zeros(0, np.int8)}
     from engine import BatchedSelfPlay
 
     n_slots = n_slots or min(num_games, 4096)
@@ -80,4 +126,16 @@ def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, strea
                          d4_augment=d4_augment, dtype=dtype,
                          sample_capacity=num_games * 130,
                          leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
-    return sp.play_games(num_games)
+    sp.play_games(num_games)
+    return sp.engine.samples()
+
+
+def _rows_to_tuples(rows):
+    """Sample rows -> the reference's [(state int8 (8,8), pi float32 (65,), G float)] with
+    state = the canonical board (own stones +1, self_play_worker.py:72)."""
+    from engine import samples_to_tuples
+
+    return samples_to_tuples({"own": np.asarray(rows["own"]).view(np.uint64),
+                              "opp": np.asarray(rows["opp"]).view(np.uint64),
+                              "pi": np.asarray(rows["pi"], np.float32),
+                              "z": np.asarray(rows["z"], np.float64)})

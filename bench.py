@@ -67,9 +67,9 @@ MFMA32_PEAK = 157.3        # dense fp32 MFMA TFLOP/s
 L2_PEAK_TBPS = 34.5        # aggregate L2 bandwidth, 8 XCDs x 4 MiB (MI355X_MICROARCH.md)
 DTYPE_LABEL = {
     "split3": "fp32-accurate net (trunk: fp32 operands split into 3 bf16 words, 6 bf16 MFMA "
-              "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
+              "partial products, fp32 accumulation; error <= 2x the fp32 MFMA kernel's vs fp64), int64 bitboards",
     "fp16x2": "fp32-accurate net (trunk: fp32 operands as scaled fp16 hi+lo pairs, 3 fp16 MFMA "
-              "partial products, fp32 accumulation; error <= fp32 MFMA's vs fp64), int64 bitboards",
+              "partial products, fp32 accumulation; error <= 2x the fp32 MFMA kernel's vs fp64), int64 bitboards",
     "fp32": "fp32 (net), int64 bitboards",
     "fp16": "fp16 trunk operands, fp32 accumulation (net), int64 bitboards",
 }
@@ -85,13 +85,18 @@ def parse():
     ap.add_argument("--warmup-exact", action="store_true",
                     help="run exactly --warmup untimed steps, not the steady-state minimum "
                          "(short profiler runs; the value is then not steady state)")
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"],
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5", "arena"],
                     help="BASELINE.json configs: c2 = configs[1], 4096 games x 100 sims "
                          "FastOthelloNet; c3 = configs[2], 1024 games x 400 sims "
                          "AlphaZeroNet(5x128) fp32 (the metric's config, default); c4 = "
                          "configs[3], 4096 games per GPU x 400 sims AlphaZeroNet(5x128) fp32 "
                          "(32,768 on 8 GPUs, RCCL all-gather); c5 = configs[4], c4 + fused D4 "
-                         "symmetry per leaf + fp16 inference")
+                         "symmetry per leaf + fp16 inference; arena = eval.py's play_match / "
+                         "evaluate_models_parallel (SURVEY 8(f)1) on configs[2]'s net and sims: "
+                         "--matches matches of two random-init AlphaZeroNet(5x128), temperature "
+                         "0, colours alternating, the reference's 4 search workers")
+    ap.add_argument("--matches", type=int, default=1024,
+                    help="arena workload: matches played (and concurrent, one wave)")
     ap.add_argument("--games", type=int, default=None, help="concurrent games per GPU")
     ap.add_argument("--leaves", type=int, default=1,
                     help="virtual-loss leaves per game per step (the reference's num_threads; "
@@ -125,6 +130,7 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "oth_step_traffic.json"))
     a = ap.parse_args()
     preset = {"c2": (4096, 100, "fast", False, "fp32"), "c3": (1024, 400, "az5x128", False, "fp32"),
+              "arena": (1024, 400, "az5x128", False, "fp32"),
               "c4": (4096, 400, "az5x128", False, "fp32"),
               "c5": (4096, 400, "az5x128", True, "fp16")}[a.workload]
     a.games = a.games or preset[0]
@@ -585,8 +591,59 @@ def aggregate_stats(allst, sims_per_move):
                          for r in allst]}
 
 
+def main_arena(a):
+    """eval.py's evaluate_models_parallel (eval.py:47-74) with play_match (:134-178) per match,
+    as arena.BatchedArena plays it: matches/s.  Two random-init nets of configs[2]'s
+    architecture, 400 sims, no num_threads in args (the reference's default of 4 workers =
+    4 virtual-loss leaves per searching slot per step), temperature 0, colours alternating.
+    A warm-up wave at 8 sims captures the search graphs first (the graphs do not depend on
+    the simulation count); the timed region is one arena.play over --matches matches."""
+    from arena import BatchedArena
+    from Models import AlphaZeroNet
+
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    torch.manual_seed(0)
+    net_a = AlphaZeroNet(8, 65, 5, 128)
+    torch.manual_seed(1)
+    net_b = AlphaZeroNet(8, 65, 5, 128)
+    args = {"c_puct": 2.0, "num_simulations": a.sims}
+    n = a.matches
+    arena = BatchedArena(net_a, net_b, args, n, device=device, seed=1234)
+    np.random.seed(0)
+    arena.args = dict(args, num_simulations=8)
+    arena.play(n)  # warm-up: the same wave layout, so every graph of the timed run exists
+    arena.args = args
+    torch.cuda.synchronize()
+    it0 = arena.iterations
+    t0 = time.perf_counter()
+    wa, wb, dr, plies = arena.play(n)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    its = arena.iterations - it0
+    result = {
+        "metric": f"arena matches/sec (eval.py play_match), 8x8 Othello @ {a.sims} MCTS sims/move",
+        "value": round(n / dt, 4), "unit": "matches/s", "n_gpus": 1, "steps": its,
+        "warmup": 1, "ms_per_step": round(dt * 1000.0 / max(1, its), 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": DTYPE_LABEL[a.conv_precision],
+        "data": "synthetic: matches from the initial position, two random-init nets",
+        "config": {"workload": "SURVEY 8(f)1 arena: eval.py evaluate_models_parallel on the "
+                               "GPU engine, configs[2]'s AlphaZeroNet(5x128) fp32 and sims",
+                   "matches": n, "sims": a.sims, "leaves_per_step": arena.K,
+                   "hip_graph": arena.use_graph, "graphs": len(arena._graphs)},
+        "value_basis": "matches / wall seconds of one arena.play (a step = one select -> net "
+                       "-> expand iteration of every searching engine)",
+        "detail": {"wins_a": wa, "wins_b": wb, "draws": dr,
+                   "mean_plies": round(float(np.mean(plies)), 2), "window_s": round(dt, 3),
+                   "iterations": its}}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     a = parse()
+    if a.workload == "arena":
+        return main_arena(a)
     if os.environ.get("AZ_FAULTHANDLER"):  # diagnostics: every thread's Python stack on a fault
         import faulthandler
 

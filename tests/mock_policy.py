@@ -84,3 +84,31 @@ def mock_eval_torch(planes, salt=0):
     h = torch.remainder(x @ At, 1021.0) + 1.0
     k = torch.remainder(x @ Bt, 2001.0)
     return (h / 1024.0).float().contiguous(), ((k - 1000.0) / 1024.0).float().contiguous()
+
+
+def MockNet(salt=0):
+    """The mock policy (salt: mock_eval's distinct "nets") as a module BatchedSelfPlay evaluates (fold=False, evaluate_planes), its
+    matrices resident on the device so the step is graph-capturable (mock_eval_torch's closed
+    form, exact in float64)."""
+    import torch
+
+    class _MockNet(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            A, B = _mats(salt)
+            self.register_buffer("At", torch.as_tensor(A.T, dtype=torch.float64))
+            self.register_buffer("Bt", torch.as_tensor(B, dtype=torch.float64))
+
+        def evaluate_planes(self, planes):
+            x = torch.round(planes.double()) + 1.0
+            h = torch.remainder(x @ self.At, 1021.0) + 1.0
+            k = torch.remainder(x @ self.Bt, 2001.0)
+            return ((h / 1024.0).float().contiguous(),
+                    ((k - 1000.0) / 1024.0).float().contiguous())
+
+        def evaluate_into(self, planes, priors, values):
+            p, v = self.evaluate_planes(planes)
+            priors.copy_(p)
+            values.copy_(v)
+
+    return _MockNet()

@@ -86,3 +86,29 @@ def test_evaluate_models_batched_with_nets():
     ps = (FastOthelloNet, net.get_config(), net.state_dict())
     a, b = evaluate_models_batched(8, {"c_puct": 2.0, "num_simulations": 8}, ps, ps, n_matches=6)
     assert 0.0 <= a <= 1.0 and 0.0 <= b <= 1.0 and a + b <= 1.0
+
+
+@pytest.mark.parametrize("threads", [None, 1])
+def test_arena_graph_replay_equals_oracle(threads):
+    """The graph-replayed search (nets with evaluate_into: select -> net on the searching
+    half's rows -> expand, captured once per plan) plays exactly the oracle's matches, with
+    more matches than slots (two waves)."""
+    from mock_policy import MockNet
+
+    args = {"c_puct": 2.0, "num_simulations": 24}
+    if threads is not None:
+        args["num_threads"] = threads
+    arena = BatchedArena(MockNet(1).cuda(), MockNet(2).cuda(), args, n_slots=6,
+                         tie_break=tie_break_lowest)
+    assert arena.use_graph
+    wa, wb, dr, plies = arena.play(10)
+    assert arena._graphs  # the searches ran from captured graphs
+    exp = [0, 0, 0]
+    exp_plies = []
+    for m in range(10):
+        a_first = m % 2 == 0
+        r, pl = oracle_play_match(1 if a_first else 2, 2 if a_first else 1, args)
+        exp_plies.append(pl)
+        exp[2 if r == 0 else (0 if (r == 1) == a_first else 1)] += 1
+    assert (wa, wb, dr) == tuple(exp)
+    assert plies == exp_plies

@@ -9,32 +9,12 @@ import numpy as np
 import pytest
 import torch
 
-from mock_policy import mock_eval_torch
+from mock_policy import MockNet, mock_eval_torch
 
 pytestmark = pytest.mark.gpu
 
 nat = pytest.importorskip("az_native")
 from engine import BatchedSelfPlay  # noqa: E402
-
-
-class MockNet(torch.nn.Module):
-    """The deterministic mock policy as a module BatchedSelfPlay evaluates (fold=False), its
-    matrices resident on the device so the step is graph-capturable (mock_eval_torch's
-    closed form, exact in float64)."""
-
-    def __init__(self):
-        super().__init__()
-        from mock_policy import _mats
-
-        A, B = _mats(0)
-        self.register_buffer("At", torch.as_tensor(A.T, dtype=torch.float64))
-        self.register_buffer("Bt", torch.as_tensor(B, dtype=torch.float64))
-
-    def evaluate_planes(self, planes):
-        x = torch.round(planes.double()) + 1.0
-        h = torch.remainder(x @ self.At, 1021.0) + 1.0
-        k = torch.remainder(x @ self.Bt, 2001.0)
-        return (h / 1024.0).float().contiguous(), ((k - 1000.0) / 1024.0).float().contiguous()
 
 
 def _run(defer, G, sims, steps, use_graph, leaves=1, fuse=True):

@@ -149,3 +149,62 @@ def test_bench_stats_fallback_plies_and_cpu_calibration_gate():
     assert bench.calibration_for(cal, "az5x128", 400, "X", 256) is None  # other CPU count
     assert bench.calibration_for(cal, "fast", 400, "X", 8) is None
     assert 1 <= bench.host_cpu_share() <= (os.cpu_count() or 1)
+
+
+def _collect_worker(rank, world, port, q, num_games):
+    """self_play_worker.collect_self_play_games under a world-`world` gloo group, the GPU
+    games replaced by synthetic engine rows (7 rows per game, tagged by rank and stream)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "alphazero-othello_amd"))
+    import self_play_worker as spw
+    from Models import FastOthelloNet
+
+    calls = []
+
+    def fake_local_rows(policy, args, n, n_slots, seed, stream_id, d4, dtype):
+        calls.append((n, stream_id, float(policy.fc_value2.weight.sum())))
+        return _rows(100 * rank + stream_id, 7 * n)
+
+    spw._local_rows = fake_local_rows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(rank)  # different weights per rank until the broadcast
+    out = spw.collect_self_play_games(FastOthelloNet(8, 65), {"num_simulations": 4}, num_games,
+                                      stream_id=10)
+    q.put((rank, calls, [(s.copy(), pi.copy(), z) for s, pi, z in out]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_collect_self_play_games_world2():
+    """One generation over two ranks: games split 3 / 2, stream_id + rank, rank 0's weights on
+    both ranks, and every rank returning the same pooled tuples in rank order (SURVEY.md
+    8(e); reference train.py:199-225)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "alphazero-othello_amd"))
+    from self_play_worker import _rows_to_tuples
+
+    world, num_games = 2, 5
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_collect_worker, args=(r, world, port, q, num_games))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, c0, out0), (_, c1, out1) = res
+    assert [c[:2] for c in c0] == [(3, 10)] and [c[:2] for c in c1] == [(2, 11)]
+    assert c0[0][2] == c1[0][2]  # the broadcast best net on both ranks
+    want = _rows_to_tuples({k: np.concatenate([_rows(10, 21)[k], _rows(111, 14)[k]])
+                            for k in ("own", "opp", "pi", "z")})
+    assert len(out0) == len(out1) == len(want) == 35
+    for a, b, w in zip(out0, out1, want):
+        for x, y, v in zip(a, b, w):
+            assert np.array_equal(x, v) and np.array_equal(y, v)

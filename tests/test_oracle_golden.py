@@ -205,6 +205,33 @@ def test_selfplay_games_match_reference(game):
         assert z == d["z"][sel][t]
 
 
+@pytest.mark.parametrize("game", [0, 3, 4, 5])
+def test_deep_selfplay_games_match_reference(game):
+    """selfplay_deep.npz (make_deep_goldens.py): 400-simulation games with one worker, and
+    games under the forced K = 4 worker schedule -- the oracle's K-leaf self-play without a
+    descent cap is that schedule."""
+    d = load_golden("selfplay_deep.npz")
+    sims, seed, plies, K = d["meta"][game]
+    lo, hi = d["log_offsets"][game], d["log_offsets"][game + 1]
+    nlo, nhi = d["noise_offsets"][game], d["noise_offsets"][game + 1]
+    rng = LogRng(d["log_kind"][lo:hi], d["log_a"][lo:hi], d["log_b"][lo:hi],
+                 d["noise"][nlo:nhi])
+    mp = MockPolicy()
+
+    def evaluate(own, opp, player):
+        return mp.inference(ob.to_state(own, opp, player), player)
+
+    samples, _ = play_game(_selfplay_args(int(sims)), evaluate, rng=rng,
+                           leaves_per_step=int(K))
+    sel = d["game"] == game
+    assert len(samples) == plies == sel.sum()
+    for t, (s, pi, z) in enumerate(samples):
+        pos, neg = ob.to_bitboards(s, 1)
+        assert pos == d["pos"][sel][t] and neg == d["neg"][sel][t]
+        assert (pi.astype(np.float32) == d["pi"][sel][t]).all()
+        assert z == d["z"][sel][t]
+
+
 def test_training_data_matches_reference():
     rows = load_golden("training_data.npz")["rows"]
     for case in np.unique(rows[:, 0]):
