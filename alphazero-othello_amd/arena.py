@@ -166,7 +166,7 @@ class BatchedArena:
         plies = []
         for base in range(0, n_matches, self.G):
             n = min(self.G, n_matches - base)
-            # colours alternate by match index (eval.py:105-112: even -> A first); slot s of
+            # colours alternate by match index (eval.py:114-121: even -> A first); slot s of
             # the wave holds match perm[s], the matches where A plays first in the first
             # slots, so each net's searching slots at a ply are one half
             a_first_m = (np.arange(base, base + n) % 2) == 0

@@ -796,17 +796,25 @@ struct HeadsOut {
 };
 
 // Last trunk conv with AlphaZeroNet's heads fused (HEADS): both output halves, final
-// (bias, residual, ReLU) in the Y registers, go to an LDS image of the four boards
-// [board][square][C] fp32 (128 KiB over the loop's buffers, free after the barrier), and
-// waves 0-3 run the heads on it (heads_az.h: the same code and registers as the stand-alone
-// heads kernel on the same values, so priors and values are bit-identical to that path)
-// while the trunk output never goes to global memory.
+// (bias, residual, ReLU) in the Y registers, go to an LDS image of the workgroup's NB boards
+// [board][square][C] fp32 (NB x 32 KiB over the loop's buffers, free after the barrier), and
+// waves 0-3 run the heads on it (heads_az.h: the same code, FC quarters and summation order
+// as the stand-alone heads kernel on the same values, so priors and values are
+// bit-identical to that path) while the trunk output never goes to global memory.  NB = 2:
+// the two-board workgroup of the default trunk conv (four waves, two workgroups per CU);
+// NB = 4: the four-board workgroup (eight waves, waves 4-7 only meet the barriers).
 template <class G>
 __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int rt0, int h,
                                                int co) {
-  constexpr int C = G::C;
-  static_assert(G::BOARDS == azh::kBoards && G::THREADS >= 64 * azh::kBoards, "heads layout");
-  static_assert(4 * 64 * C * 4 + 3 * 1024 <= G::LDS_BYTES, "heads LDS");
+  constexpr int C = G::C, NB = G::BOARDS;
+  constexpr int IMG = NB * 64 * C * 4;  // the image; p [NB][128] and v [NB][64] after it
+  static_assert(NB <= azh::kQuarters && G::THREADS >= 64 * azh::kQuarters, "heads layout");
+  static_assert(IMG + NB * (128 + 64) * 4 <= G::LDS_BYTES, "heads LDS");
+  // the partial sums (lp at 0, hv at 4,352) overlay the image's first board, written after
+  // heads_four's first barrier, when no wave reads the image any more
+  static_assert(azh::kQuarters * NB * 65 * 4 <= 4352 &&
+                    4352 + azh::kQuarters * NB * 64 * 16 <= IMG,
+                "heads scratch inside the image");
   float* img = reinterpret_cast<float*>(S.lds);
   __syncthreads();  // every wave is past its loop and its staged-residual reads
 #pragma unroll
@@ -824,19 +832,18 @@ __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int
     }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool active = wave < azh::kBoards, live = active && wave < S.nb;
-  // a missing board (last workgroup) reads board 0's row: computed, never stored
+  const bool active = wave < azh::kQuarters, live = wave < NB && wave < S.nb;
+  // a missing board (last workgroup) or a quarter-only wave reads board 0's row: computed
+  // by the 1x1 convs only for waves < NB, never stored
   const float4* hp =
       reinterpret_cast<const float4*>(img + ((live ? wave : 0) * 64 + lane) * C);
-  // p / v after the image (written while other waves still read it); the partial sums
-  // over the image's start (written after heads_four's first barrier)
   char* base = S.lds;
-  const azh::Scratch L{reinterpret_cast<float(*)[128]>(base + 4 * 64 * C * 4),
-                       reinterpret_cast<float(*)[64]>(base + 4 * 64 * C * 4 + 2048),
-                       reinterpret_cast<float(*)[azh::kBoards][65]>(base),
-                       reinterpret_cast<float4(*)[azh::kBoards][64]>(base + 4352)};
-  azh::heads_four<C>([&](int c) { return hp[c]; }, lane, wave & (azh::kBoards - 1), S.b0 + wave,
-                     live, active, ho.w, L, ho.priors, ho.values);
+  const azh::ScratchT<NB> L{reinterpret_cast<float(*)[128]>(base + IMG),
+                            reinterpret_cast<float(*)[64]>(base + IMG + NB * 128 * 4),
+                            reinterpret_cast<float(*)[NB][65]>(base),
+                            reinterpret_cast<float4(*)[NB][64]>(base + 4352)};
+  azh::heads_four<C, NB>([&](int c) { return hp[c]; }, lane, wave & (azh::kQuarters - 1),
+                         S.b0 + wave, live, active, ho.w, L, ho.priors, ho.values);
 }
 
 // One conv of this workgroup's boards (the whole kernel of k_conv3x3_wino4; the persistent
@@ -1319,6 +1326,26 @@ extern "C" int az_w4_stamps(unsigned long long* host, int n) {
 }
 #endif
 
+namespace {
+template <class G>
+int launch_wino4_heads(const float* x, const void* wq, const float* bias, const float* res,
+                       int n_boards, float* in_absmax, const HeadsOut& ho, void* stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_conv3x3_wino4<G, true, true, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true, true>), dim3(grid), dim3(G::THREADS),
+                     (size_t)G::LDS_BYTES, azc::as_stream(stream), x,
+                     static_cast<const char*>(wq), bias, res, nullptr, n_boards, in_absmax,
+                     nullptr, ho);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+}  // namespace
+
 extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const float* bias,
                                           const float* res, int32_t n_boards,
                                           int32_t channels, int32_t mode, float* in_absmax,
@@ -1340,25 +1367,17 @@ extern "C" int az_conv3x3_wino4_heads_gpu(const float* x, const void* wq, const 
   AZ_REQUIRE(channels == 128 && mode == AZ_CONV_FP16X2, AZ_ERR_ARG,
              "az_conv3x3_wino4_heads_gpu: 128 channels in FP16X2 mode only (got %d, mode %d)",
              channels, mode);
-  // four boards per workgroup, one workgroup per CU (not the two-board default of
-  // az_conv3x3_wino4_gpu: with two co-resident two-board workgroups this epilogue's values
-  // differed from the separate heads kernel's on ~0.3 % of boards, exact with one per CU --
-  // profiles/r03_heads_two_board.json)
-  using G = W4<AZ_CONV_FP16X2, 1>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    AZ_HIP(hipFuncSetAttribute((const void*)k_conv3x3_wino4<G, true, true, true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
-    attr_set = true;
-  }
+  // AZ_W4_HEADS_BOARDS: 2 = two-board workgroups, two per CU (the trunk conv's default
+  // form), 4 = four-board workgroups, one per CU (the round-3 form); read per call so the
+  // tests compare the two
+  const char* hbe = getenv("AZ_W4_HEADS_BOARDS");
+  const int hb = hbe ? atoi(hbe) : 2;
+  AZ_REQUIRE(hb == 2 || hb == 4, AZ_ERR_ARG, "AZ_W4_HEADS_BOARDS must be 2 or 4, got %d", hb);
   const HeadsOut ho{{wpv, bpv, wpolT, bpol, w1T, b1, w2, b2}, priors, values};
-  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
-  hipLaunchKernelGGL((k_conv3x3_wino4<G, true, true, true>), dim3(grid), dim3(G::THREADS),
-                     (size_t)G::LDS_BYTES, azc::as_stream(stream), x,
-                     static_cast<const char*>(wq), bias, res, nullptr, n_boards, in_absmax,
-                     nullptr, ho);
-  AZ_HIP(hipGetLastError());
-  return AZ_OK;
+  if (hb == 2) return launch_wino4_heads<W4<AZ_CONV_FP16X2, 1, 2>>(x, wq, bias, res, n_boards,
+                                                                    in_absmax, ho, stream);
+  return launch_wino4_heads<W4<AZ_CONV_FP16X2, 1>>(x, wq, bias, res, n_boards, in_absmax, ho,
+                                                   stream);
 }
 
 extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias,

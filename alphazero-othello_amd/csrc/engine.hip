@@ -139,6 +139,9 @@ struct Games {
   uint8_t* sym;        // [G, K] D4 transform of each pending leaf
   int32_t* noise_cur;  // injected-stream cursors
   int32_t* u_cur;
+  // K > 1 auto-play: leaves of a batch still open when the launch's descent cap stopped it
+  // (rows 0 .. open - 1 hold them, their virtual loss applied; 0 = no open batch)
+  int32_t* open;
   // trajectory [G, T]
   uint64_t* t_own;
   uint64_t* t_opp;
@@ -708,6 +711,26 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const Params* __restrict__
     w.path[j] = -1;
     plane[j] = 0.0f;
   }
+  int open0 = 0;
+  if constexpr (KMAX > 1) {
+    // an open batch (the last launch's descent cap stopped it before K leaves waited):
+    // its leaves keep their rows and virtual loss, and this launch's descents continue it --
+    // the reference's schedule (a batch = simulations started until K wait on the net) is
+    // the same wherever launches split it
+    open0 = p.g.open[g];
+    if (open0 > 0) {
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        if (j < open0) {
+          const int64_t row = row0 + j;
+          const int plen = p.g.path_len[row];
+          w.path[j] = lane < plen ? p.g.path[row * kMaxPath + lane] : -1;
+          plane[j] = nn_in[row * 64 + lane];
+        }
+      }
+      w.n = open0;
+    }
+  }
   bool deep = false;  // a waiting path past kMaxPath: its virtual loss could not be tracked
   int depth = 0;      // depth of the current node
   int path_node = 0;  // lane d: node at depth d of the current descent
@@ -814,6 +837,12 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const Params* __restrict__
     if (deep) {
       p.g.overflow[g] += 1;
       atomicAdd(&p.ctr->overflow, 1ull);
+    }
+    if constexpr (KMAX > 1) {
+      // stopped by the descent cap with fewer than K leaves waiting and simulations left:
+      // the batch stays open (expansion skips it; the next select continues it)
+      const int op = p.auto_play && w.n > 0 && w.n < K && sims_done + w.n < target ? w.n : 0;
+      if (op != open0) p.g.open[g] = op;
     }
   }
   ENG_STAMP(3);
@@ -1047,13 +1076,14 @@ __device__ __forceinline__ bool expand_slot(const Params& p, int g,
   const int half = p.g.half[g];
   int n_nodes = p.g.n_nodes[g];
   const int sd0 = p.g.sims_done[g], target = p.g.sims_target[g];
+  const int open = KMAX > 1 ? p.g.open[g] : 0;
   LeafIn in[KMAX];
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < K) in[j] = load_leaf_in(p, row0 + j, priors, values);
   // every load above in flight before any is waited for (the compiler would otherwise sink
   // them past the early exit below, one dependent round trip each)
-  asm volatile("" ::"v"(half), "v"(n_nodes), "v"(sd0), "v"(target));
+  asm volatile("" ::"v"(half), "v"(n_nodes), "v"(sd0), "v"(target), "v"(open));
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < K)
@@ -1061,7 +1091,9 @@ __device__ __forceinline__ bool expand_slot(const Params& p, int g,
                    "v"(in[j].pr64), "v"(in[j].v), "v"(in[j].sym));
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) in[j].sym = p.d4 ? in[j].sym : 0;
-  if (in[0].leaf < 0) return false;
+  // a batch the last select left open (its descent cap) waits for more leaves: the next
+  // select continues it, and its leaves are expanded once it closes
+  if (in[0].leaf < 0 || open > 0) return false;
   double done_v[KMAX];
   int n_sims = 0;
 #pragma unroll
@@ -1442,6 +1474,7 @@ __device__ void new_game(const Params& p, int g) {
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = p.sims;
   p.g.leaf[(int64_t)g * p.K] = -1;
+  p.g.open[g] = 0;
   p.g.status[g] = kActive;
 }
 
@@ -1775,6 +1808,7 @@ __global__ void k_set_root(const Params* __restrict__ pp, int g, uint64_t own, u
   p.g.n_nodes[g] = 1;
   p.g.root_player[g] = player;
   p.g.leaf[(int64_t)g * p.K] = -1;
+  p.g.open[g] = 0;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = 0;
   p.g.status[g] = kSearchDone;
@@ -1788,6 +1822,7 @@ __global__ void k_begin(const Params* __restrict__ pp, int slot, int sims) {
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = sims;
   p.g.leaf[(int64_t)g * p.K] = -1;
+  p.g.open[g] = 0;
   p.g.status[g] = kActive;
 }
 
@@ -1860,6 +1895,7 @@ __global__ void k_set_roots(const Params* __restrict__ pp, const int32_t* slots,
   p.g.n_nodes[g] = 1;
   p.g.root_player[g] = player[i];
   p.g.leaf[(int64_t)g * p.K] = -1;
+  p.g.open[g] = 0;
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = 0;
   p.g.status[g] = kSearchDone;
@@ -1874,6 +1910,7 @@ __global__ void k_begin_slots(const Params* __restrict__ pp, const int32_t* slot
   p.g.sims_done[g] = 0;
   p.g.sims_target[g] = sims;
   p.g.leaf[(int64_t)g * p.K] = -1;
+  p.g.open[g] = 0;
   p.g.status[g] = kActive;
 }
 
@@ -2107,6 +2144,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
   chk(dalloc(e, &p.g.sym, GK));
   chk(dalloc(e, &p.g.noise_cur, G));
   chk(dalloc(e, &p.g.u_cur, G));
+  chk(dalloc(e, &p.g.open, G));
   chk(dalloc(e, &p.g.t_own, G * T));
   chk(dalloc(e, &p.g.t_opp, G * T));
   chk(dalloc(e, &p.g.t_pi, G * T * 65));
@@ -2192,7 +2230,7 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
                  hipMemset(p.a.nchild, 0, nodes) == hipSuccess;
   for (int32_t* a : {p.g.status, p.g.half, p.g.n_nodes, p.g.sims_done, p.g.sims_target,
                      p.g.ply, p.g.root_player, p.g.winner, p.g.overflow,
-                     p.g.start_step, p.g.sstep, p.g.noise_cur, p.g.u_cur})
+                     p.g.start_step, p.g.sstep, p.g.noise_cur, p.g.u_cur, p.g.open})
     zero_ok = zero_ok && hipMemset(a, 0, G * sizeof(int32_t)) == hipSuccess;
   zero_ok = zero_ok && hipMemset(p.g.sims_acc, 0, G * sizeof(unsigned long long)) == hipSuccess &&
             hipMemset(p.g.rng_event, 0, G * sizeof(uint32_t)) == hipSuccess &&
@@ -2271,8 +2309,8 @@ static int launch_select(az_engine* e, float* nn_in, int32_t* leaf_o, int par, i
     const char* v = getenv("AZ_MAX_DESCENTS");  // experiment knob (scripts/exp), default 4
     return v ? atoi(v) : 0;
   }();
-  // (with K leaves per step the cap is 4 K descents: a step that reaches it waits on fewer
-  // leaves, another legal interleaving of the reference's workers)
+  // (with K leaves per step the cap is 4 K descents: a launch that reaches it with fewer than
+  // K leaves waiting leaves its batch open for the next launch -- the same batches)
   const int max_descents = e->p.auto_play ? (env_md > 0 ? env_md : 4 * e->p.K)
                                           : 4 * (e->p.sims + 1) + 64;
   const dim3 grid(sel_grid(e) + (unsigned)move_blocks);

@@ -1,5 +1,5 @@
-// heads_az.h — AlphaZeroNet's policy and value heads for four boards, one wavefront per
-// board, shared by the stand-alone heads kernel (heads.hip, trunk output read from global
+// heads_az.h — AlphaZeroNet's policy and value heads for NB = 4 (or 2) boards of a
+// workgroup's four waves, one wavefront per board for the 1x1 convs, shared by the stand-alone heads kernel (heads.hip, trunk output read from global
 // memory) and the last trunk conv with the heads fused into its epilogue (conv_wino4.hip,
 // trunk output read from LDS).  Both feed the same registers to the same code, so the two
 // paths give bit-identical priors and values.
@@ -10,16 +10,18 @@
 //   v = relu(conv1x1_{C->1}(h) + b)            v[pos]
 //   value = tanh(val_fc2(relu(val_fc1(v))))   (64 -> 256 -> 1)
 // Lane = board square for the 1x1 convs.  The FCs are split by INPUT range over the four
-// waves, each computing its quarter for all four boards (pol_fc^T [128][65]: inputs
+// waves, each computing its quarter for all NB boards (pol_fc^T [128][65]: inputs
 // 32w..32w+31; val_fc1^T [64][256]: inputs 16w..16w+15), so every FC weight is read from L2
-// once per four boards; the partial sums meet in LDS and wave b adds them in order for
-// board b.
+// once per NB boards; the partial sums meet in LDS and wave b adds them in order for
+// board b.  The quarters and their order do not depend on NB, so every NB gives the same
+// bits (the two-board form is the fused epilogue of the two-board trunk conv).
 #pragma once
 #include <hip/hip_runtime.h>
 
 namespace azh {
 
-constexpr int kBoards = 4;  // boards (= computing waves) per workgroup
+constexpr int kBoards = 4;  // boards per workgroup of the stand-alone kernel
+constexpr int kQuarters = 4;  // waves splitting the FC inputs (any NB <= 4 boards)
 
 struct Weights {
   const float* wpv;    // [3][C]: policy ch 0, policy ch 1, value
@@ -32,15 +34,17 @@ struct Weights {
   const float* b2;     // [1]
 };
 
-// LDS the four waves exchange partial sums through (3 KiB + 20.3 KiB); `p` / `v` are
-// written while other waves may still be reading their activations, the rest only after
-// the first barrier
-struct Scratch {
-  float (*p)[128];             // [kBoards][128] relu'd policy 1x1 conv, NCHW-flat
-  float (*v)[64];              // [kBoards][64] relu'd value 1x1 conv
-  float (*lp)[kBoards][65];    // [wave][board][logit] partial logits
-  float4 (*hv)[kBoards][64];   // [wave][board][lane] partial val_fc1 hidden units
+// LDS the four waves exchange partial sums through (NB = 4: 3 KiB + 20.3 KiB); `p` / `v`
+// are written while other waves may still be reading their activations, the rest only
+// after the first barrier
+template <int NB = kBoards>
+struct ScratchT {
+  float (*p)[128];             // [NB][128] relu'd policy 1x1 conv, NCHW-flat
+  float (*v)[64];              // [NB][64] relu'd value 1x1 conv
+  float (*lp)[NB][65];         // [quarter][board][logit] partial logits
+  float4 (*hv)[NB][64];        // [quarter][board][lane] partial val_fc1 hidden units
 };
+using Scratch = ScratchT<kBoards>;
 
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
@@ -53,16 +57,18 @@ __device__ __forceinline__ float wave_max(float x) {
   return x;
 }
 
-// Wave w of the workgroup (w < kBoards computes; any further waves of a larger workgroup
-// pass active = false and only take part in the two barriers): xf(c) = channels 4c..4c+3
-// of board w's activations at square `lane` (registers loaded up front, or LDS read on
-// demand), b = that board's index, live = it exists.
-template <int C, class XF>
+// Wave w < 4 of the workgroup computes FC quarter w (any further waves of a larger
+// workgroup pass active = false and only take part in the two barriers); waves w < NB also
+// own board w: xf(c) = channels 4c..4c+3 of board w's activations at square `lane`
+// (registers loaded up front, or LDS read on demand), b = that board's index, live = it
+// exists (false for w >= NB).
+template <int C, int NB = kBoards, class XF>
 __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool live,
-                                           bool active, const Weights& W, const Scratch& L,
-                                           float* __restrict__ priors,
+                                           bool active, const Weights& W,
+                                           const ScratchT<NB>& L, float* __restrict__ priors,
                                            float* __restrict__ values) {
-  constexpr int KP = 128 / kBoards, KV = 64 / kBoards;  // FC inputs per wave
+  static_assert(NB >= 1 && NB <= kQuarters, "boards per workgroup");
+  constexpr int KP = 128 / kQuarters, KV = 64 / kQuarters;  // FC inputs per wave
   float wpl[KP];
   float w64 = 0.f;
   float4 wq[KV];
@@ -73,7 +79,9 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
 #pragma unroll
     for (int i = 0; i < KV; ++i)
       wq[i] = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
-    // 1x1 convs (policy 2 channels, value 1 channel) at square `lane`
+  }
+  if (active && w < NB) {
+    // 1x1 convs (policy 2 channels, value 1 channel) of board w at square `lane`
     float d0 = 0.f, d1 = 0.f, d2 = 0.f;
     const float4* w0 = reinterpret_cast<const float4*>(W.wpv);
     const float4* w1 = reinterpret_cast<const float4*>(W.wpv + C);
@@ -94,7 +102,7 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
   // this wave's input quarter of both FCs, for every board of the workgroup
   if (active) {
 #pragma unroll
-    for (int bd = 0; bd < kBoards; ++bd) {
+    for (int bd = 0; bd < NB; ++bd) {
       float la = 0.f;
 #pragma unroll
       for (int k = 0; k < KP; ++k) la += wpl[k] * L.p[bd][KP * w + k];
@@ -114,12 +122,12 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
     }
   }
   __syncthreads();
-  if (!active || !live) return;  // whole wave (b is uniform per wave); no barrier follows
+  if (!active || !live || w >= NB) return;  // whole wave (uniform); no barrier follows
 
   // board w: the quarters added in order, softmax over the 65 logits
   float la = W.bpol[lane], l64 = W.bpol[64];
 #pragma unroll
-  for (int q = 0; q < kBoards; ++q) {
+  for (int q = 0; q < kQuarters; ++q) {
     la += L.lp[q][w][lane];
     l64 += L.lp[q][w][64];
   }
@@ -132,7 +140,7 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
   // value: lane j -> hidden units 4j..4j+3 of val_fc1, then val_fc2 reduced over the wave
   float4 acc = reinterpret_cast<const float4*>(W.b1)[lane];
 #pragma unroll
-  for (int q = 0; q < kBoards; ++q) {
+  for (int q = 0; q < kQuarters; ++q) {
     const float4 a = L.hv[q][w][lane];
     acc.x += a.x;
     acc.y += a.y;

@@ -98,10 +98,9 @@ class SeqMCTS:
     """Flat-array tree; node 0 is the root after every re-root."""
 
     def __init__(self, c_puct, num_simulations, evaluate=None, dirichlet_alpha=0.03,
-                 dirichlet_epsilon=0.0, rng=None, leaves_per_step=1, max_descents=None):
+                 dirichlet_epsilon=0.0, rng=None, leaves_per_step=1):
         self.c_puct = c_puct
         self.K = max(1, int(leaves_per_step))
-        self.max_descents = max_descents  # per step (the engine's auto-play cap), None = no cap
         self.sims = num_simulations
         self.evaluate = evaluate  # (own, opp, player) -> (priors f32[65], value float)
         self.alpha = dirichlet_alpha
@@ -233,11 +232,11 @@ class SeqMCTS:
         return kids[best]
 
     def simulate_batch(self, remaining):
-        """One engine step of the K-leaf search: returns the simulations it completed."""
-        done, pending, vv, descents = 0, [], {}, 0
-        cap = self.max_descents or float("inf")
-        while done + len(pending) < remaining and len(pending) < self.K and descents < cap:
-            descents += 1
+        """One batch of the K-leaf search (simulations started one after another until K wait
+        on the evaluation or none remain; the interleaving make_vl_goldens.py forces on the
+        reference's workers): returns the simulations it completed."""
+        done, pending, vv = 0, [], {}
+        while done + len(pending) < remaining and len(pending) < self.K:
             i, path = self.root, []
             while True:
                 path.append(i)

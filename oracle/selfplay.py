@@ -28,14 +28,14 @@ def td_lambda_targets(players, v_roots, winner, lambd):
     return out
 
 
-def play_game(args, evaluate, rng=None, max_plies=200, leaves_per_step=1, max_descents=None):
+def play_game(args, evaluate, rng=None, max_plies=200, leaves_per_step=1):
     """One self-play game; returns (samples, winner) where samples are
     (canonical int8 (8,8), pi float32[65], target float) as one_self_play returns."""
     rng = rng or NumpyRng()
     m = SeqMCTS(args["c_puct"], args["num_simulations"], evaluate,
                 dirichlet_alpha=args["dirichlet_alpha"],
                 dirichlet_epsilon=args["dirichlet_epsilon"], rng=rng,
-                leaves_per_step=leaves_per_step, max_descents=max_descents)
+                leaves_per_step=leaves_per_step)
     game = ob.OracleGame()
     state = game.get_initial_state()
     player = 1

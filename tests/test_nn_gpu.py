@@ -450,19 +450,22 @@ def test_persistent_trunk_bit_identical_to_layer_launches(B, heads, monkeypatch)
     assert not torch.isnan(out[True][0]).any()
 
 
+@pytest.mark.parametrize("heads_boards", ["2", "4"])
 @pytest.mark.parametrize("boards", ["2", "4"])
 @pytest.mark.parametrize("B", [257, 1024, 1030, 4096])
-def test_fused_heads_bit_identical_to_separate_heads(B, boards, monkeypatch):
+def test_fused_heads_bit_identical_to_separate_heads(B, boards, heads_boards, monkeypatch):
     """AlphaZeroNet on the fp16x2 trunk: the heads fused into the last conv's epilogue
     (az_conv3x3_wino4_heads_gpu, the trunk output kept in LDS) give the same priors and
     values, bit for bit, as the last conv followed by the separate heads kernel
     (az_heads_az_gpu): heads_az.h runs the same code on the same fp32 values.  Ragged
     batches (a partial last workgroup) included, with two-board (default) and four-board
     (AZ_W4_BOARDS=4) workgroups: heads_az.h adds the FC input quarters in the same order
-    for any number of boards per workgroup."""
+    for any number of boards per workgroup; the heads-fused conv itself in both forms
+    (AZ_W4_HEADS_BOARDS: two-board workgroups two per CU, the default, or four-board)."""
     from Models import FusedInferenceNet
 
     monkeypatch.setenv("AZ_W4_BOARDS", boards)
+    monkeypatch.setenv("AZ_W4_HEADS_BOARDS", heads_boards)
 
     torch.manual_seed(3)
     net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
@@ -484,3 +487,34 @@ def test_fused_heads_bit_identical_to_separate_heads(B, boards, monkeypatch):
         logits, v = net(x.view(-1, 1, 8, 8))
     torch.testing.assert_close(out[True][0], torch.softmax(logits, -1), atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(out[True][1], v.reshape(-1), atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1024, 1030])
+def test_two_board_fused_heads_stress(B, monkeypatch):
+    """Two co-resident two-board heads-fused workgroups per CU (the default last conv) over
+    repeated evaluations of the persistent-trunk tower: every launch's priors and values bit
+    for bit equal to the separate heads kernel's (round 3 saw a timing-dependent value
+    difference on 1-6 boards per launch in an earlier two-board epilogue)."""
+    from Models import FusedInferenceNet
+
+    monkeypatch.setenv("AZ_W4_HEADS_BOARDS", "2")
+    torch.manual_seed(11)
+    net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    monkeypatch.setattr(FusedInferenceNet, "fuse_heads", False)
+    ref_p = torch.empty(B, 65, device="cuda")
+    ref_v = torch.empty(B, device="cuda")
+    with torch.no_grad():
+        fused.evaluate_into(x, ref_p, ref_v)
+    monkeypatch.setattr(FusedInferenceNet, "fuse_heads", True)
+    reps = 60
+    pr = torch.full((reps, B, 65), float("nan"), device="cuda")
+    va = torch.full((reps, B), float("nan"), device="cuda")
+    with torch.no_grad():
+        for i in range(reps):
+            fused.evaluate_into(x, pr[i], va[i])
+    torch.cuda.synchronize()
+    bad_v = (va != ref_v).any(0).nonzero().flatten().tolist()
+    bad_p = (pr != ref_p).any(2).any(0).nonzero().flatten().tolist()
+    assert not bad_v and not bad_p, (bad_v[:16], bad_p[:16])

@@ -134,7 +134,7 @@ def test_virtual_loss_self_play_matches_oracle():
     games, streams = [], []
     for s in range(G):
         rng = _GenRng(700 + s)
-        samples, _ = play_game(args, evaluate, rng=rng, leaves_per_step=K, max_descents=4 * K)
+        samples, _ = play_game(args, evaluate, rng=rng, leaves_per_step=K)
         games.append(samples)
         streams.append(engine_streams(rng.kinds, rng.a, rng.b,
                                       np.array(rng.noise).reshape(-1, 65)))
