@@ -660,6 +660,8 @@ class FusedInferenceNet(nn.Module, Inference):
         import az_native as nat
 
         C = c1s[0].channels
+        if heads_into is not None and self.trunk_heads:
+            return self._trunk4_heads(h, bufs, c1s, heads_into, planes)
         if planes is not None:
             B = planes.shape[0]
             planes = planes.reshape(B, 64).contiguous()
@@ -681,6 +683,37 @@ class FusedInferenceNet(nn.Module, Inference):
             c2s[-1].forward_heads(t, h_last, bufs[1], self._hw, *heads_into)
             return None
         return h_last
+
+    # AZ_TRUNK_HEADS (default on): the heads-fused last conv inside the persistent trunk's
+    # launch (az_trunk_wino4_heads_gpu) instead of a launch of its own after it; 0 = the
+    # separate az_conv3x3_wino4_heads_gpu launch (bit-identical)
+    trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "1") != "0"
+
+    def _trunk4_heads(self, h, bufs, c1s, heads_into, planes=None):
+        """The whole tower and the heads in one az_trunk_wino4_heads_gpu launch."""
+        import az_native as nat
+
+        C = c1s[0].channels
+        if planes is not None:
+            B = planes.shape[0]
+            planes = planes.reshape(B, 64).contiguous()
+            h = torch.empty((B, C, 8, 8), dtype=torch.float32, device=planes.device,
+                            memory_format=torch.channels_last)
+        B = h.shape[0]
+        hb = [torch.empty_like(h, memory_format=torch.channels_last) for _ in range(2)]
+        t = torch.empty_like(h, memory_format=torch.channels_last)
+        st = self.stem if planes is not None else None
+        hw = self._hw
+        priors, values = heads_into
+        nat.check(nat.lib.az_trunk_wino4_heads_gpu(
+            nat.ptr(self._t4["wq"]), nat.ptr(self._t4["bias"]), nat.ptr(planes),
+            nat.ptr(st.w9) if st is not None else None, nat.ptr(st.bias) if st is not None else None,
+            nat.ptr(h), nat.ptr(hb[0]), nat.ptr(hb[1]), nat.ptr(t), nat.ptr(bufs[0]),
+            nat.ptr(bufs[1]), B, 2 * len(c1s), C, nat.ptr(hw["wpv"]), nat.ptr(hw["bpv"]),
+            nat.ptr(hw["wpolT"]), nat.ptr(hw["bpol"]), nat.ptr(hw["w1T"]), nat.ptr(hw["b1"]),
+            nat.ptr(hw["w2"]), nat.ptr(hw["b2"]), nat.ptr(priors), nat.ptr(values),
+            nat.stream_ptr()), "az_trunk_wino4_heads_gpu")
+        return None
 
     def _fused_heads_ready(self):
         if self.kind != "az" or self.conv_impl != "hip":

@@ -1071,6 +1071,9 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_conv3x3_wino4(
 // drained (vmcnt(0)) and an L1 invalidate (buffer_inv sc0: the ping-pong buffers were read
 // by earlier layers) order it; per-board ranges ping-pong amax[0] / amax[1] as between the
 // per-layer launches.  Same arithmetic per layer: bit-identical to those launches.
+#ifndef AZ_W4_STAGGER
+#define AZ_W4_STAGGER 0
+#endif
 struct TrunkW4 {
   const char* const* wq;     // [n_convs] prepared weights (layer order)
   const float* const* bias;  // [n_convs]
@@ -1137,8 +1140,51 @@ __device__ __forceinline__ void stem_board(const float* __restrict__ planes,
   if (tid == 0) absmax[b] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
 }
 
+// AlphaZeroNet's heads on this workgroup's NB boards of the tower's output y (just written
+// by this workgroup, after a layer_fence): heads_four with each board's activations read on
+// demand from y (L2), its partial sums in the workgroup's LDS -- the same code and order as
+// the separate heads kernel, so bit-identical priors / values.
 template <class G>
-__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a) {
+__device__ __forceinline__ void trunk_heads(const float* __restrict__ y, int n_boards,
+                                            const HeadsOut& ho) {
+  constexpr int C = G::C, NB = G::BOARDS;
+  static_assert(NB <= azh::kQuarters && G::THREADS >= 64 * azh::kQuarters, "heads layout");
+  extern __shared__ float4 lds4[];
+  char* base = reinterpret_cast<char*>(lds4);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b0 = blockIdx.x * NB;
+  const int nb = n_boards - b0 < NB ? n_boards - b0 : NB;
+  const bool active = wave < azh::kQuarters, live = wave < NB && wave < nb;
+  const float4* hp = reinterpret_cast<const float4*>(
+      y + ((size_t)(b0 + (live ? wave : 0)) * 64 + lane) * C);
+  // p [NB][128] at 0, v [NB][64] at 1 KiB, lp [4][NB][65] at 2 KiB, hv [4][NB][64] at 4,352
+  static_assert(NB * 128 * 4 <= 1024 && 1024 + NB * 64 * 4 <= 2048 &&
+                    2048 + azh::kQuarters * NB * 65 * 4 <= 4352,
+                "heads scratch layout");
+  const azh::ScratchT<NB> L{reinterpret_cast<float(*)[128]>(base),
+                            reinterpret_cast<float(*)[64]>(base + 1024),
+                            reinterpret_cast<float(*)[NB][65]>(base + 2048),
+                            reinterpret_cast<float4(*)[NB][64]>(base + 4352)};
+  azh::heads_four<C, NB>([&](int c) { return hp[c]; }, lane, wave & (azh::kQuarters - 1),
+                         b0 + wave, live, active, ho.w, L, ho.priors, ho.values);
+}
+
+// HEADS: after the last conv (n_convs - 1, a block's second: odd; its output stored as in
+// any layer) each workgroup runs AlphaZeroNet's heads on its boards (trunk_heads: priors /
+// values bit-identical to az_conv3x3_wino4_heads_gpu and to the separate heads kernel) --
+// the tower and the heads in one launch, no kernel boundary before the last layer.  (The
+// heads in the last conv's epilogue, inlined here as a third body, spilled ~100 VGPRs into
+// the layer loop.)
+template <class G, bool HEADS = false>
+__global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a,
+                                                                      HeadsOut ho) {
+#if AZ_W4_STAGGER
+  // experiment: the second half of the grid (the second workgroup on each CU when every
+  // workgroup is resident) starts later, so the two co-resident workgroups' phases differ
+  if (blockIdx.x >= (gridDim.x + 1) / 2) {
+    for (int i = 0; i < AZ_W4_STAGGER; ++i) __builtin_amdgcn_s_sleep(8);  // 512 clocks each
+  }
+#endif
   if (a.planes) {  // the stem of this workgroup's boards first (its output never leaves L2)
     static_assert(G::THREADS == 256 && G::C == 128, "stem_board's mapping");
     extern __shared__ float4 lds4[];
@@ -1156,11 +1202,19 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
       conv_body<G, false, true, false, true>(h, a.wq[i], a.bias[i], nullptr, a.t, a.n_boards,
                                              a.amax[0], a.amax[1], HeadsOut{});
     } else {
+      // the last layer of a HEADS launch keeps no range (nothing reads its output as a
+      // conv input): amax[0] stays as the stem / caller left it
+      const bool last_heads = HEADS && i == a.n_convs - 1;
       conv_body<G, true, true, false, true>(a.t, a.wq[i], a.bias[i], h, a.hb[ob], a.n_boards,
-                                            a.amax[1], a.amax[0], HeadsOut{});
+                                            a.amax[1], last_heads ? nullptr : a.amax[0],
+                                            HeadsOut{});
       h = a.hb[ob];
       ob ^= 1;
     }
+  }
+  if constexpr (HEADS) {
+    layer_fence();  // the last layer's stores drained and visible to this workgroup's reads
+    trunk_heads<G>(h, a.n_boards, ho);
   }
 }
 
@@ -1412,7 +1466,54 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
                   {amax0, amax1}, planes, stem_w, stem_b, n_boards, n_convs};
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
   hipLaunchKernelGGL((k_trunk_wino4<G>), dim3(grid), dim3(G::THREADS), (size_t)G::LDS_BYTES,
-                     azc::as_stream(stream), a);
+                     azc::as_stream(stream), a, HeadsOut{});
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* const* bias,
+                                        const float* planes, const float* stem_w,
+                                        const float* stem_b, float* h_in, float* hb0,
+                                        float* hb1, float* t, float* amax0, float* amax1,
+                                        int32_t n_boards, int32_t n_convs, int32_t channels,
+                                        const float* wpv, const float* bpv,
+                                        const float* wpolT, const float* bpol,
+                                        const float* w1T, const float* b1, const float* w2,
+                                        const float* b2, float* priors, float* values,
+                                        void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && n_boards <= kW4MaxBoards && n_convs >= 2 && n_convs % 2 == 0,
+             AZ_ERR_ARG,
+             "az_trunk_wino4_heads_gpu: n_boards %d (<= %d) / n_convs %d (even, >= 2)", n_boards,
+             kW4MaxBoards, n_convs);
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(wq && bias && h_in && hb0 && hb1 && t && amax0 && amax1, AZ_ERR_ARG,
+             "az_trunk_wino4_heads_gpu: null buffer");
+  AZ_REQUIRE(h_in != hb0 && h_in != hb1 && h_in != t && hb0 != hb1 && hb0 != t && hb1 != t &&
+                 amax0 != amax1,
+             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: aliased buffers");
+  AZ_REQUIRE(((uintptr_t)h_in | (uintptr_t)hb0 | (uintptr_t)hb1 | (uintptr_t)t) % 16 == 0,
+             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(channels == 128, AZ_ERR_ARG,
+             "az_trunk_wino4_heads_gpu: channels must be 128, got %d", channels);
+  AZ_REQUIRE(!planes || (stem_w && stem_b && ((uintptr_t)stem_w | (uintptr_t)stem_b) % 16 == 0),
+             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: planes without 16-byte aligned stem weights");
+  AZ_REQUIRE(wpv && bpv && wpolT && bpol && w1T && b1 && w2 && b2 && priors && values,
+             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: null heads buffer");
+  AZ_REQUIRE(((uintptr_t)wpv | (uintptr_t)w1T | (uintptr_t)b1 | (uintptr_t)w2) % 16 == 0,
+             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: heads weights must be 16-byte aligned");
+  using G = W4<AZ_CONV_FP16X2, 1, 2>;  // two-board workgroups, FP16X2
+  static bool attr_set = false;
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+    attr_set = true;
+  }
+  const TrunkW4 a{reinterpret_cast<const char* const*>(wq), bias, h_in, {hb0, hb1}, t,
+                  {amax0, amax1}, planes, stem_w, stem_b, n_boards, n_convs};
+  const HeadsOut ho{{wpv, bpv, wpolT, bpol, w1T, b1, w2, b2}, priors, values};
+  const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
+  hipLaunchKernelGGL((k_trunk_wino4<G, true>), dim3(grid), dim3(G::THREADS),
+                     (size_t)G::LDS_BYTES, azc::as_stream(stream), a, ho);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

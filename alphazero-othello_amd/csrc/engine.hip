@@ -768,8 +768,11 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const Params* __restrict__
     }
     w.n = j + 1;
   };
+  // the root's own expansion (an unexplored root) is a batch of its own, never left open
+  bool root_wait = false;
   if (!(rec_flags(cur) & kExpanded)) {
     wait_leaf();  // policy_improve_step expands an unexplored root first (MCTS_model.py:234-235)
+    root_wait = true;
   } else {
     int guard = 0;
     // tree levels walked by this launch's descents: the level budget (AZ_SEL_LEVELS, K = 1)
@@ -841,7 +844,8 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const Params* __restrict__
     if constexpr (KMAX > 1) {
       // stopped by the descent cap with fewer than K leaves waiting and simulations left:
       // the batch stays open (expansion skips it; the next select continues it)
-      const int op = p.auto_play && w.n > 0 && w.n < K && sims_done + w.n < target ? w.n : 0;
+      const int op =
+          p.auto_play && !root_wait && w.n > 0 && w.n < K && sims_done + w.n < target ? w.n : 0;
       if (op != open0) p.g.open[g] = op;
     }
   }

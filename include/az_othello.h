@@ -458,6 +458,22 @@ int az_trunk_wino4_gpu(const void* const* wq, const float* const* bias, const fl
                        float* hb1, float* t, float* amax0, float* amax1, int32_t n_boards,
                        int32_t n_convs, int32_t channels, void* stream);
 
+/* az_trunk_wino4_gpu with the tower's last conv (n_convs even: every block, the last
+ * block's second conv included) running AlphaZeroNet's policy / value heads in its epilogue,
+ * exactly az_conv3x3_wino4_heads_gpu's (heads weights and outputs as there): the whole net
+ * after the stem in one launch, the last layer's output never stored.  priors [n][65] /
+ * values [n] bit-identical to az_trunk_wino4_gpu (n_convs - 1) + az_conv3x3_wino4_heads_gpu
+ * and to the separate az_heads_az_gpu.  Replaces reference Models.py:205-221
+ * (AlphaZeroNet.forward after conv0) + the softmax of MCTS_model.py:319. */
+int az_trunk_wino4_heads_gpu(const void* const* wq, const float* const* bias,
+                             const float* planes, const float* stem_w, const float* stem_b,
+                             float* h_in, float* hb0, float* hb1, float* t, float* amax0,
+                             float* amax1, int32_t n_boards, int32_t n_convs, int32_t channels,
+                             const float* wpv, const float* bpv, const float* wpolT,
+                             const float* bpol, const float* w1T, const float* b1,
+                             const float* w2, const float* b2, float* priors, float* values,
+                             void* stream);
+
 /* ---------------- replay buffer (device) -------------------------------------------
  * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with
  * equal (own, opp, version) — the reference's (sha1(canonical int8 board), version) —

@@ -518,3 +518,32 @@ def test_two_board_fused_heads_stress(B, monkeypatch):
     bad_v = (va != ref_v).any(0).nonzero().flatten().tolist()
     bad_p = (pr != ref_p).any(2).any(0).nonzero().flatten().tolist()
     assert not bad_v and not bad_p, (bad_v[:16], bad_p[:16])
+
+
+@pytest.mark.parametrize("B", [257, 1023, 1024])
+def test_trunk_heads_bit_identical(B, monkeypatch):
+    """The whole tower and the heads in one persistent launch (az_trunk_wino4_heads_gpu)
+    against the tower launch + the heads-fused conv launch, and against the separate heads
+    kernel: priors and values bit for bit, repeated launches."""
+    from Models import FusedInferenceNet
+
+    torch.manual_seed(7)
+    net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    out = {}
+    for name, fh, th in (("separate", False, False), ("conv", True, False), ("trunk", True, True)):
+        monkeypatch.setattr(FusedInferenceNet, "fuse_heads", fh)
+        monkeypatch.setattr(FusedInferenceNet, "trunk_heads", th)
+        reps = 20 if name == "trunk" else 1
+        pr = torch.full((reps, B, 65), float("nan"), device="cuda")
+        va = torch.full((reps, B), float("nan"), device="cuda")
+        with torch.no_grad():
+            for i in range(reps):
+                fused.evaluate_into(x, pr[i], va[i])
+        torch.cuda.synchronize()
+        out[name] = (pr, va)
+    for name in ("conv", "trunk"):
+        pr, va = out[name]
+        assert torch.equal(pr, out["separate"][0].expand_as(pr)), name
+        assert torch.equal(va, out["separate"][1].expand_as(va)), name
