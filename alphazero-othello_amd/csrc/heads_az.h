@@ -18,6 +18,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef AZ_HEADS_CHECK
+#define AZ_HEADS_CHECK 0
+#endif
+
 namespace azh {
 
 constexpr int kBoards = 4;  // boards per workgroup of the stand-alone kernel
@@ -80,6 +84,9 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
     for (int i = 0; i < KV; ++i)
       wq[i] = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
   }
+#if AZ_HEADS_CHECK
+  float myv = 0.f;  // debug builds: this wave's own value 1x1 output, kept in a register
+#endif
   if (active && w < NB) {
     // 1x1 convs (policy 2 channels, value 1 channel) of board w at square `lane`
     float d0 = 0.f, d1 = 0.f, d2 = 0.f;
@@ -96,6 +103,9 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
     L.p[w][lane] = fmaxf(d0 + W.bpv[0], 0.f);
     L.p[w][64 + lane] = fmaxf(d1 + W.bpv[1], 0.f);
     L.v[w][lane] = fmaxf(d2 + W.bpv[2], 0.f);
+#if AZ_HEADS_CHECK
+    myv = fmaxf(d2 + W.bpv[2], 0.f);
+#endif
   }
   __syncthreads();
 
@@ -152,6 +162,39 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
                      fmaxf(acc.z, 0.f) * o.z + fmaxf(acc.w, 0.f) * o.w;
   const float val = wave_sum(part) + W.b2[0];
   if (lane == 0) values[b] = tanhf(val);
+#if AZ_HEADS_CHECK
+  // debug builds: the value path recomputed by this wave alone from its own registers (no
+  // LDS), in the same order; every differing word named
+  if (L.v[w][lane] != myv)
+    printf("HEADS_CHECK v wg %d wave %d board %d lane %d lds %a reg %a\n", (int)blockIdx.x,
+           (int)(threadIdx.x >> 6), b, lane, L.v[w][lane], myv);
+  float4 chk = reinterpret_cast<const float4*>(W.b1)[lane];
+  for (int q = 0; q < kQuarters; ++q) {
+    float4 pq = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < KV; ++i) {
+      const float vi = __shfl(myv, KV * q + i, 64);
+      const float4 wi = reinterpret_cast<const float4*>(W.w1T + (KV * q + i) * 256)[lane];
+      pq.x += wi.x * vi;
+      pq.y += wi.y * vi;
+      pq.z += wi.z * vi;
+      pq.w += wi.w * vi;
+    }
+    const float4 a = L.hv[q][w][lane];
+    if (a.x != pq.x || a.y != pq.y || a.z != pq.z || a.w != pq.w)
+      printf("HEADS_CHECK hv wg %d wave %d board %d q %d lane %d lds %a %a reg %a %a\n",
+             (int)blockIdx.x, (int)(threadIdx.x >> 6), b, q, lane, a.x, a.y, pq.x, pq.y);
+    chk.x += pq.x;
+    chk.y += pq.y;
+    chk.z += pq.z;
+    chk.w += pq.w;
+  }
+  const float part2 = fmaxf(chk.x, 0.f) * o.x + fmaxf(chk.y, 0.f) * o.y +
+                      fmaxf(chk.z, 0.f) * o.z + fmaxf(chk.w, 0.f) * o.w;
+  const float val2 = wave_sum(part2) + W.b2[0];
+  if (lane == 0 && val2 != val)
+    printf("HEADS_CHECK val wg %d wave %d board %d lds %a reg %a\n", (int)blockIdx.x,
+           (int)(threadIdx.x >> 6), b, val, val2);
+#endif
 }
 
 }  // namespace azh
