@@ -50,6 +50,18 @@ struct ScratchT {
 };
 using Scratch = ScratchT<kBoards>;
 
+// Wait for this wave's LDS stores before their data registers are rewritten.  Observed on
+// gfx950 (round 4, AZ_HEADS_CHECK build, profiles/r04_heads_war.json): with two two-board
+// workgroups on a CU, the compiler's `ds_write_b128 v81, v[90:93]` of a partial-sum quad,
+// followed two instructions later by `ds_read_b128 v[90:93], ...` into the same registers,
+// stored wrong words for lanes 48-63 -- the last 16 lanes' data read from the registers after
+// the load had overwritten them -- on a few boards per launch (never with one workgroup per
+// CU, i.e. only under LDS data-path contention).  Waiting on lgkmcnt before the registers
+// are reused closes that window.
+__device__ __forceinline__ void lds_store_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
@@ -129,6 +141,9 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
         acc.w += wq[i].w * vi;
       }
       L.hv[w][bd][lane] = acc;
+      // the store's data registers are reused by the next LDS reads at once: wait for it
+      // here (lds_store_wait) -- see below
+      lds_store_wait();
     }
   }
   __syncthreads();
