@@ -144,6 +144,29 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
       // the store's data registers are reused by the next LDS reads at once: wait for it
       // here (lds_store_wait) -- see below
       lds_store_wait();
+#if AZ_HEADS_CHECK
+      {  // debug builds: the quad recomputed from fresh weight loads, and read back
+        float4 acc2 = {0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < KV; ++i) {
+          const float vi = L.v[bd][KV * w + i];
+          const float4 wi = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
+          acc2.x += wi.x * vi;
+          acc2.y += wi.y * vi;
+          acc2.z += wi.z * vi;
+          acc2.w += wi.w * vi;
+          if (wi.x != wq[i].x || wi.y != wq[i].y || wi.z != wq[i].z || wi.w != wq[i].w)
+            printf("HEADS_CHECK wq wg %d wave %d q %d i %d lane %d reg %a fresh %a\n",
+                   (int)blockIdx.x, (int)(threadIdx.x >> 6), w, i, lane, wq[i].x, wi.x);
+        }
+        if (acc2.x != acc.x || acc2.y != acc.y || acc2.z != acc.z || acc2.w != acc.w)
+          printf("HEADS_CHECK acc wg %d wave %d q %d bd %d lane %d reg %a fresh %a\n",
+                 (int)blockIdx.x, (int)(threadIdx.x >> 6), w, bd, lane, acc.x, acc2.x);
+        const float4 rb = L.hv[w][bd][lane];
+        if (rb.x != acc.x || rb.y != acc.y || rb.z != acc.z || rb.w != acc.w)
+          printf("HEADS_CHECK store wg %d wave %d q %d bd %d lane %d lds %a reg %a\n",
+                 (int)blockIdx.x, (int)(threadIdx.x >> 6), w, bd, lane, rb.x, acc.x);
+      }
+#endif
     }
   }
   __syncthreads();
