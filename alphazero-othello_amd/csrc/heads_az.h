@@ -21,6 +21,9 @@
 #ifndef AZ_HEADS_CHECK
 #define AZ_HEADS_CHECK 0
 #endif
+#ifndef AZ_HEADS_FIX
+#define AZ_HEADS_FIX 0
+#endif
 
 namespace azh {
 
@@ -95,6 +98,15 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
 #pragma unroll
     for (int i = 0; i < KV; ++i)
       wq[i] = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
+#if AZ_HEADS_FIX & 1
+    // experiment: every FC weight in its registers (vmcnt(0) and a pause) before first use
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < KV; ++i)
+      asm volatile("" : "+v"(wq[i].x), "+v"(wq[i].y), "+v"(wq[i].z), "+v"(wq[i].w));
+#pragma unroll
+    for (int k = 0; k < KP; ++k) asm volatile("" : "+v"(wpl[k]));
+#endif
   }
 #if AZ_HEADS_CHECK
   float myv = 0.f;  // debug builds: this wave's own value 1x1 output, kept in a register
@@ -139,6 +151,10 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
         acc.y += wq[i].y * vi;
         acc.z += wq[i].z * vi;
         acc.w += wq[i].w * vi;
+#if AZ_HEADS_FIX & 2
+        // experiment: each component its own chain (no packed f32 pairing)
+        asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w));
+#endif
       }
       L.hv[w][bd][lane] = acc;
       // the store's data registers are reused by the next LDS reads at once: wait for it
