@@ -21,9 +21,7 @@
 #ifndef AZ_HEADS_CHECK
 #define AZ_HEADS_CHECK 0
 #endif
-#ifndef AZ_HEADS_FIX
-#define AZ_HEADS_FIX 0
-#endif
+
 
 namespace azh {
 
@@ -53,16 +51,19 @@ struct ScratchT {
 };
 using Scratch = ScratchT<kBoards>;
 
-// Wait for this wave's LDS stores before their data registers are rewritten.  Observed on
-// gfx950 (round 4, AZ_HEADS_CHECK build, profiles/r04_heads_war.json): with two two-board
-// workgroups on a CU, the compiler's `ds_write_b128 v81, v[90:93]` of a partial-sum quad,
-// followed two instructions later by `ds_read_b128 v[90:93], ...` into the same registers,
-// stored wrong words for lanes 48-63 -- the last 16 lanes' data read from the registers after
-// the load had overwritten them -- on a few boards per launch (never with one workgroup per
-// CU, i.e. only under LDS data-path contention).  Waiting on lgkmcnt before the registers
-// are reused closes that window.
-__device__ __forceinline__ void lds_store_wait() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+// The four components of a float4 accumulator kept as four separate fp32 chains.  Left to
+// itself the compiler pairs them into v_pk_mul_f32 / v_pk_add_f32 (SLP); in the val_fc1
+// partial sums below those packed chains gave wrong words -- in lanes 48-63 only, in a few
+// boards per launch, and only with two two-board workgroups resident on a CU (round 3's
+// "values, never priors" on the two-board heads).  Located in round 4 with the AZ_HEADS_CHECK
+// build (every wave recomputes its value path from its own registers and names each
+// differing word: only lanes 48-63 of the partial-sum quads, profiles/r04_heads_war.json);
+// an A/B of fixes (profiles/r04_heads_fix_ab.json): waiting for the FC weights before use
+// leaves the errors, unpaired chains (this) remove them in every heads test and stress run.
+// An empty asm with the four values as read-write operands stops the pairing; the float
+// operations and their order are unchanged.
+__device__ __forceinline__ void unpaired(float4& a) {
+  asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
 }
 
 __device__ __forceinline__ float wave_sum(float x) {
@@ -98,15 +99,6 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
 #pragma unroll
     for (int i = 0; i < KV; ++i)
       wq[i] = reinterpret_cast<const float4*>(W.w1T + (KV * w + i) * 256)[lane];
-#if AZ_HEADS_FIX & 1
-    // experiment: every FC weight in its registers (vmcnt(0) and a pause) before first use
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < KV; ++i)
-      asm volatile("" : "+v"(wq[i].x), "+v"(wq[i].y), "+v"(wq[i].z), "+v"(wq[i].w));
-#pragma unroll
-    for (int k = 0; k < KP; ++k) asm volatile("" : "+v"(wpl[k]));
-#endif
   }
 #if AZ_HEADS_CHECK
   float myv = 0.f;  // debug builds: this wave's own value 1x1 output, kept in a register
@@ -151,15 +143,9 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
         acc.y += wq[i].y * vi;
         acc.z += wq[i].z * vi;
         acc.w += wq[i].w * vi;
-#if AZ_HEADS_FIX & 2
-        // experiment: each component its own chain (no packed f32 pairing)
-        asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w));
-#endif
+        unpaired(acc);
       }
       L.hv[w][bd][lane] = acc;
-      // the store's data registers are reused by the next LDS reads at once: wait for it
-      // here (lds_store_wait) -- see below
-      lds_store_wait();
 #if AZ_HEADS_CHECK
       {  // debug builds: the quad recomputed from fresh weight loads, and read back
         float4 acc2 = {0.f, 0.f, 0.f, 0.f};
@@ -210,6 +196,7 @@ __device__ __forceinline__ void heads_four(XF&& xf, int lane, int w, int b, bool
     acc.y += a.y;
     acc.z += a.z;
     acc.w += a.w;
+    unpaired(acc);
   }
   const float4 o = reinterpret_cast<const float4*>(W.w2)[lane];
   const float part = fmaxf(acc.x, 0.f) * o.x + fmaxf(acc.y, 0.f) * o.y +
