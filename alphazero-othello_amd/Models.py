@@ -684,10 +684,12 @@ class FusedInferenceNet(nn.Module, Inference):
             return None
         return h_last
 
-    # AZ_TRUNK_HEADS (default on): the heads-fused last conv inside the persistent trunk's
-    # launch (az_trunk_wino4_heads_gpu) instead of a launch of its own after it; 0 = the
-    # separate az_conv3x3_wino4_heads_gpu launch (bit-identical)
-    trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "1") != "0"
+    # AZ_TRUNK_HEADS=1: the heads inside the persistent trunk's launch, after its last conv
+    # (az_trunk_wino4_heads_gpu, bit-identical) instead of the heads-fused last conv as a
+    # launch of its own.  Off: B = 1,024 evaluation 449-451 vs 445-446 us, configs[2] bench
+    # 96.6-96.8 vs 97.6 games/s same box (profiles/r04_net_ab.json) -- the last layer's output
+    # then makes an L2 round trip the fused epilogue avoids
+    trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "0") == "1"
 
     def _trunk4_heads(self, h, bufs, c1s, heads_into, planes=None):
         """The whole tower and the heads in one az_trunk_wino4_heads_gpu launch."""

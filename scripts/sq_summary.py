@@ -1,6 +1,7 @@
 """Average per-dispatch counter values of rocprofv3 --pmc CSVs (gpurun_out/sq_<tag>_<pass>/),
 skipping the first dispatches (warm-up): python scripts/sq_summary.py gpurun_out/sq_wino4_fp16"""
 import csv
+import os
 import glob
 import sys
 from collections import defaultdict
@@ -11,7 +12,7 @@ for prefix in sys.argv[1:]:
         rows = list(csv.DictReader(open(f)))
         per = defaultdict(lambda: defaultdict(float))
         for r in rows:
-            if "conv3x3" not in r["Kernel_Name"]:
+            if os.environ.get("SQ_KERNEL", "conv3x3") not in r["Kernel_Name"]:
                 continue
             per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         ids = sorted(per)[5:]
