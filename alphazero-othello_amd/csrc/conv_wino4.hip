@@ -1087,6 +1087,20 @@ struct TrunkW4 {
   int n_boards, n_convs;
 };
 
+// a pointer loaded from device memory (the per-layer weight / bias tables) as a wave-uniform
+// value: the compiler loads it with a vector load (the kernel writes global memory, so no
+// scalar load) and cannot prove the result uniform, so every buffer descriptor built from it
+// became divergent and each buffer load ran in a waterfall loop (v_readfirstlane /
+// v_cmp_eq_u64 / s_and_saveexec per load: 1,540 readfirstlanes in the kernel, 1.7x the
+// standalone conv's VALU per conv -- profiles/r04_trunk_sq_counters.txt)
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ void layer_fence() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\tbuffer_inv sc0" ::: "memory");
 }
@@ -1199,13 +1213,15 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   for (int i = 0; i < a.n_convs; ++i) {
     if (i > 0) layer_fence();
     if ((i & 1) == 0) {
-      conv_body<G, false, true, false, true>(h, a.wq[i], a.bias[i], nullptr, a.t, a.n_boards,
+      conv_body<G, false, true, false, true>(h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]),
+                                             nullptr, a.t, a.n_boards,
                                              a.amax[0], a.amax[1], HeadsOut{});
     } else {
       // the last layer of a HEADS launch keeps no range (nothing reads its output as a
       // conv input): amax[0] stays as the stem / caller left it
       const bool last_heads = HEADS && i == a.n_convs - 1;
-      conv_body<G, true, true, false, true>(a.t, a.wq[i], a.bias[i], h, a.hb[ob], a.n_boards,
+      conv_body<G, true, true, false, true>(a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h,
+                                            a.hb[ob], a.n_boards,
                                             a.amax[1], last_heads ? nullptr : a.amax[0],
                                             HeadsOut{});
       h = a.hb[ob];
