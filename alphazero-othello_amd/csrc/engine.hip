@@ -646,14 +646,13 @@ __device__ __forceinline__ bool expand_slot(const Params& p, int g,
 // the slot sits this step out, so each of its moves lands one step later than with k_expand;
 // which step a move lands in never changes a game.
 template <int KMAX, bool MERGED = false, bool FUSED = false>
-__global__ __launch_bounds__(kSelBlock) void k_select(const Params* __restrict__ pp,
+__global__ __launch_bounds__(kSelBlock) void k_select(Params p,
                                                       float* __restrict__ nn_in,
                                                       int32_t* __restrict__ leaf_o,
                                                       int max_descents, int par,
                                                       int move_blocks,
                                                       const float* __restrict__ priors,
                                                       const float* __restrict__ values) {
-  const Params& p = *pp;
   if constexpr (MERGED) {  // a separate instantiation: the plain one keeps its registers
     if ((int)blockIdx.x < move_blocks) {
       move_body(p, par ^ 1, 1, move_blocks, (int)blockIdx.x);
@@ -1139,10 +1138,9 @@ __device__ __forceinline__ bool expand_slot(const Params& p, int g,
 
 // One wavefront per slot: expand_slot.
 template <int KMAX>
-__global__ __launch_bounds__(kSelBlock) void k_expand(const Params* __restrict__ pp, const float* __restrict__ priors,
+__global__ __launch_bounds__(kSelBlock) void k_expand(Params p, const float* __restrict__ priors,
                                                       const float* __restrict__ values,
                                                       int par) {
-  const Params& p = *pp;
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   ENG_STAMP_BEGIN(2);
@@ -1739,14 +1737,12 @@ __device__ __forceinline__ void move_body(const Params& p, int q, int deferred, 
   (void)deferred;
 }
 
-__global__ __launch_bounds__(kMoveBlock) void k_move(const Params* __restrict__ pp) {
-  const Params& p = *pp;
+__global__ __launch_bounds__(kMoveBlock) void k_move(Params p) {
   move_body(p, 0, 0, (int)gridDim.x, (int)blockIdx.x);
 }
 
 // ctr->sims = sum of the slots' counters (one workgroup; az_counters only)
-__global__ __launch_bounds__(1024) void k_sum_sims(const Params* __restrict__ pp) {
-  const Params& p = *pp;
+__global__ __launch_bounds__(1024) void k_sum_sims(Params p) {
   __shared__ unsigned long long s_part[1024 / kWave];
   unsigned long long v = 0;
   for (int g = threadIdx.x; g < p.G; g += blockDim.x) v += p.g.sims_acc[g];
@@ -1767,8 +1763,7 @@ __global__ void k_tick(Counters* c) { c->step += 1; }
 // ---------------------------------------------------------------------------------
 // host-driven (MCTS API) kernels
 
-__global__ void k_reset(const Params* __restrict__ pp, long long budget, int stagger) {
-  const Params& p = *pp;
+__global__ void k_reset(Params p, long long budget, int stagger) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g == 0) {
     p.ctr->games_started = 0;
@@ -1804,8 +1799,7 @@ __global__ void k_reset(const Params* __restrict__ pp, long long budget, int sta
   }
 }
 
-__global__ void k_set_root(const Params* __restrict__ pp, int g, uint64_t own, uint64_t opp, int player) {
-  const Params& p = *pp;
+__global__ void k_set_root(Params p, int g, uint64_t own, uint64_t opp, int player) {
   if (threadIdx.x != 0) return;
   p.g.half[g] = 0;
   init_root(p, g, 0, own, opp);
@@ -1818,8 +1812,7 @@ __global__ void k_set_root(const Params* __restrict__ pp, int g, uint64_t own, u
   p.g.status[g] = kSearchDone;
 }
 
-__global__ void k_begin(const Params* __restrict__ pp, int slot, int sims) {
-  const Params& p = *pp;
+__global__ void k_begin(Params p, int slot, int sims) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= p.G || (slot >= 0 && g != slot)) return;
   if (p.g.status[g] == kIdle || p.g.status[g] == kFinished) return;
@@ -1830,9 +1823,8 @@ __global__ void k_begin(const Params* __restrict__ pp, int slot, int sims) {
   p.g.status[g] = kActive;
 }
 
-__global__ void k_policy(const Params* __restrict__ pp, int slot, double temp, double u_tie, float* pi_o,
+__global__ void k_policy(Params p, int slot, double temp, double u_tie, float* pi_o,
                          double* vroot_o, int32_t* counts_o) {
-  const Params& p = *pp;
   const int g = slot;
   const int lane = threadIdx.x;
   const int half = p.g.half[g];
@@ -1858,9 +1850,8 @@ __global__ void k_policy(const Params* __restrict__ pp, int slot, double temp, d
   }
 }
 
-__global__ __launch_bounds__(kMoveBlock) void k_reroot(const Params* __restrict__ pp, int g, int action,
+__global__ __launch_bounds__(kMoveBlock) void k_reroot(Params p, int g, int action,
                                                        int32_t* result) {
-  const Params& p = *pp;
   extern __shared__ __align__(16) int32_t map[];
   __shared__ int s_child;
   const int half = p.g.half[g];
@@ -1887,9 +1878,8 @@ __global__ __launch_bounds__(kMoveBlock) void k_reroot(const Params* __restrict_
 
 // ---- batched host-driven control (arena evaluation: many independent searches) -------
 
-__global__ void k_set_roots(const Params* __restrict__ pp, const int32_t* slots, const uint64_t* own,
+__global__ void k_set_roots(Params p, const int32_t* slots, const uint64_t* own,
                             const uint64_t* opp, const int32_t* player, int n) {
-  const Params& p = *pp;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int g = slots[i];
@@ -1905,8 +1895,7 @@ __global__ void k_set_roots(const Params* __restrict__ pp, const int32_t* slots,
   p.g.status[g] = kSearchDone;
 }
 
-__global__ void k_begin_slots(const Params* __restrict__ pp, const int32_t* slots, int n, int sims) {
-  const Params& p = *pp;
+__global__ void k_begin_slots(Params p, const int32_t* slots, int n, int sims) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int g = slots[i];
@@ -1919,9 +1908,8 @@ __global__ void k_begin_slots(const Params* __restrict__ pp, const int32_t* slot
 }
 
 // child visit counts (int32 [G, 65]) and root W/N of every slot: one wave per slot
-__global__ __launch_bounds__(kSelBlock) void k_root_stats(const Params* __restrict__ pp, int32_t* counts,
+__global__ __launch_bounds__(kSelBlock) void k_root_stats(Params p, int32_t* counts,
                                                           double* vroot) {
-  const Params& p = *pp;
   const int g = blockIdx.x * (kSelBlock / kWave) + (threadIdx.x >> 6);
   if (g >= p.G) return;
   const int lane = lane_id();
@@ -1944,9 +1932,8 @@ __global__ __launch_bounds__(kSelBlock) void k_root_stats(const Params* __restri
 
 // re-root every slot with actions[g] >= 0 (MCTS.make_move on many trees at once);
 // found[g] = child node or -1 (KeyError / no tree); one workgroup per slot
-__global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(const Params* __restrict__ pp, const int32_t* actions,
+__global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(Params p, const int32_t* actions,
                                                              int32_t* found) {
-  const Params& p = *pp;
   extern __shared__ __align__(16) int32_t map[];
   __shared__ int s_child;
   for (int g = blockIdx.x; g < p.G; g += gridDim.x) {
@@ -1987,12 +1974,11 @@ __global__ __launch_bounds__(kMoveBlock) void k_reroot_slots(const Params* __res
 
 struct az_engine {
   az_config cfg;
-  Params p;  // host copy; kernels read the device snapshot dp
-  // The kernels take the engine's parameters through a pointer to an immutable device copy
-  // (a 24-byte-class kernarg instead of the ~840-byte struct by value): every change of p
-  // publishes a NEW snapshot (publish_params), so a launch or a captured HIP graph keeps
-  // reading the parameters it was issued with, exactly as with by-value arguments.
-  const Params* dp = nullptr;
+  // kernels take the parameters by value (kernarg): their pointer fields keep the global
+  // address space, so loads and stores through them are global_* instructions (through a
+  // pointer to a device copy of Params they compiled to flat_*: round 4, reverted -- it did
+  // not change the profiler faults either)
+  Params p;
   std::vector<void*> allocs;
   int32_t* d_result = nullptr;
   char* d_scratch = nullptr;  // 1 KiB: az_root_policy outputs
@@ -2031,17 +2017,6 @@ int dalloc(az_engine* e, T** ptr, size_t count) {
 void free_all(az_engine* e) {
   for (void* q : e->allocs) (void)hipFree(q);
   e->allocs.clear();
-}
-
-// a fresh device snapshot of e->p (no kernel has seen the new buffer: no synchronisation)
-int publish_params(az_engine* e) {
-  Params* d = nullptr;
-  AZ_TRY(dalloc(e, &d, 1));
-  const hipError_t err = hipMemcpy(d, &e->p, sizeof(Params), hipMemcpyHostToDevice);
-  if (err != hipSuccess)
-    return azc::set_error(AZ_ERR_HIP, "hipMemcpy(Params) failed: %s", hipGetErrorString(err));
-  e->dp = d;
-  return AZ_OK;
 }
 
 unsigned sel_grid(const az_engine* e) {
@@ -2245,12 +2220,6 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
     delete e;
     return azc::set_error(AZ_ERR_HIP, "hipMemset failed");
   }
-  rc = publish_params(e);
-  if (rc != AZ_OK) {
-    free_all(e);
-    delete e;
-    return rc;
-  }
   *out = e;
   return AZ_OK;
   AZ_GUARD_END
@@ -2268,7 +2237,7 @@ int az_reset_all(az_engine* e, int64_t start_budget, int32_t stagger_steps, void
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   hipStream_t s = azc::as_stream(stream);
   const unsigned grid = (unsigned)((e->p.G + 255) / 256);
-  hipLaunchKernelGGL(k_reset, dim3(grid), dim3(256), 0, s, e->dp, (long long)start_budget,
+  hipLaunchKernelGGL(k_reset, dim3(grid), dim3(256), 0, s, e->p, (long long)start_budget,
                      (int)stagger_steps);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipStreamSynchronize(s));
@@ -2282,7 +2251,7 @@ int az_set_root(az_engine* e, int32_t slot, uint64_t own, uint64_t opp, int32_t 
   AZ_REQUIRE((own & opp) == 0, AZ_ERR_ARG, "own and opp overlap");
   AZ_REQUIRE(player == 1 || player == -1, AZ_ERR_ARG, "player must be +1 or -1");
   hipStream_t s = azc::as_stream(stream);
-  hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, s, e->dp, (int)slot, own, opp,
+  hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, s, e->p, (int)slot, own, opp,
                      (int)player);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipStreamSynchronize(s));
@@ -2295,7 +2264,7 @@ int az_begin_search(az_engine* e, int32_t slot, int32_t num_simulations, void* s
   AZ_REQUIRE(num_simulations >= 0, AZ_ERR_ARG, "num_simulations < 0");
   hipStream_t s = azc::as_stream(stream);
   const unsigned grid = (unsigned)((e->p.G + 255) / 256);
-  hipLaunchKernelGGL(k_begin, dim3(grid), dim3(256), 0, s, e->dp, (int)slot,
+  hipLaunchKernelGGL(k_begin, dim3(grid), dim3(256), 0, s, e->p, (int)slot,
                      (int)num_simulations);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -2323,13 +2292,13 @@ static int launch_select(az_engine* e, float* nn_in, int32_t* leaf_o, int par, i
 #define AZ_SEL_GO(KM)                                                                       \
   do {                                                                                     \
     if (fused)                                                                             \
-      hipLaunchKernelGGL((k_select<KM, true, true>), grid, dim3(kSelBlock), lds, s, e->dp,   \
+      hipLaunchKernelGGL((k_select<KM, true, true>), grid, dim3(kSelBlock), lds, s, e->p,   \
                          nn_in, leaf_o, max_descents, par, move_blocks, priors, values);   \
     else if (move_blocks)                                                                  \
-      hipLaunchKernelGGL((k_select<KM, true>), grid, dim3(kSelBlock), lds, s, e->dp, nn_in,  \
+      hipLaunchKernelGGL((k_select<KM, true>), grid, dim3(kSelBlock), lds, s, e->p, nn_in,  \
                          leaf_o, max_descents, par, move_blocks, nullptr, nullptr);        \
     else                                                                                   \
-      hipLaunchKernelGGL((k_select<KM, false>), grid, dim3(kSelBlock), lds, s, e->dp, nn_in, \
+      hipLaunchKernelGGL((k_select<KM, false>), grid, dim3(kSelBlock), lds, s, e->p, nn_in, \
                          leaf_o, max_descents, par, 0, nullptr, nullptr);                  \
   } while (0)
   if (e->p.K == 1)
@@ -2357,7 +2326,7 @@ int az_engine_defer_moves(az_engine* e, int32_t on) {
   AZ_REQUIRE(e, AZ_ERR_ARG, "null engine");
   AZ_REQUIRE(e->p.auto_play || !on, AZ_ERR_STATE, "deferred moves need an auto-play engine");
   e->p.defer = on ? 1 : 0;
-  return publish_params(e);
+  return AZ_OK;
 }
 
 int az_engine_set_stem(az_engine* e, const float* w9, const float* bias, float* y,
@@ -2367,7 +2336,7 @@ int az_engine_set_stem(az_engine* e, const float* w9, const float* bias, float* 
     e->p.stem_c = 0;
     e->p.stem_w = e->p.stem_b = nullptr;
     e->p.stem_y = e->p.stem_amax = nullptr;
-    return publish_params(e);
+    return AZ_OK;
   }
   AZ_REQUIRE(channels == 64 || channels == 128, AZ_ERR_ARG,
              "az_engine_set_stem: channels must be 0, 64 or 128, got %d", channels);
@@ -2379,7 +2348,7 @@ int az_engine_set_stem(az_engine* e, const float* w9, const float* bias, float* 
   e->p.stem_y = y;
   e->p.stem_amax = absmax;
   e->p.stem_c = channels;
-  return publish_params(e);
+  return AZ_OK;
 }
 
 int az_select_move(az_engine* e, float* nn_in, int32_t* leaf_o, int32_t par, void* stream) {
@@ -2428,16 +2397,16 @@ int az_move_flush(az_engine* e, int32_t par, void* stream) {
   const dim3 grid((unsigned)mb);
   const int q = par ^ 1;
   if (e->p.K == 1)
-    hipLaunchKernelGGL((k_select<1, true>), grid, dim3(kSelBlock), e->lds_move, s, e->dp, nullptr,
+    hipLaunchKernelGGL((k_select<1, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
                        nullptr, 0, q, mb, nullptr, nullptr);
   else if (e->p.K <= 2)
-    hipLaunchKernelGGL((k_select<2, true>), grid, dim3(kSelBlock), e->lds_move, s, e->dp, nullptr,
+    hipLaunchKernelGGL((k_select<2, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
                        nullptr, 0, q, mb, nullptr, nullptr);
   else if (e->p.K <= 4)
-    hipLaunchKernelGGL((k_select<4, true>), grid, dim3(kSelBlock), e->lds_move, s, e->dp, nullptr,
+    hipLaunchKernelGGL((k_select<4, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p, nullptr,
                        nullptr, 0, q, mb, nullptr, nullptr);
   else
-    hipLaunchKernelGGL((k_select<kMaxLeaves, true>), grid, dim3(kSelBlock), e->lds_move, s, e->dp,
+    hipLaunchKernelGGL((k_select<kMaxLeaves, true>), grid, dim3(kSelBlock), e->lds_move, s, e->p,
                        nullptr, nullptr, 0, q, mb, nullptr, nullptr);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -2454,16 +2423,16 @@ static int launch_expand(az_engine* e, const float* priors, const float* values,
     values = e->d_zero_eval + (size_t)e->p.G * e->p.K * 65;
   }
   if (e->p.K == 1)
-    hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->dp, priors,
+    hipLaunchKernelGGL(k_expand<1>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
                        values, par);
   else if (e->p.K <= 2)
-    hipLaunchKernelGGL(k_expand<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->dp, priors,
+    hipLaunchKernelGGL(k_expand<2>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
                        values, par);
   else if (e->p.K <= 4)
-    hipLaunchKernelGGL(k_expand<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->dp, priors,
+    hipLaunchKernelGGL(k_expand<4>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, priors,
                        values, par);
   else
-    hipLaunchKernelGGL(k_expand<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->dp,
+    hipLaunchKernelGGL(k_expand<kMaxLeaves>, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p,
                        priors, values, par);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -2496,7 +2465,7 @@ int az_play(az_engine* e, void* stream) {
   // workgroups take them grid-stride, and each workgroup's closing atomic on the shared
   // move_done counter stays cheap (one address serialises ~90 atomics per microsecond)
   const int blocks = e->p.G < 64 ? e->p.G : 64;
-  hipLaunchKernelGGL(k_move, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->dp);
+  hipLaunchKernelGGL(k_move, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->p);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
@@ -2526,7 +2495,7 @@ int az_root_policy(az_engine* e, int32_t slot, double temp, double u_tie, float*
   float* d_pi = (float*)e->d_scratch;                  // [0, 260)
   double* d_v = (double*)(e->d_scratch + 264);          // [264, 272)
   int32_t* d_c = (int32_t*)(e->d_scratch + 272);        // [272, 532)
-  hipLaunchKernelGGL(k_policy, dim3(1), dim3(64), 0, s, e->dp, (int)slot, temp, u_tie, d_pi, d_v,
+  hipLaunchKernelGGL(k_policy, dim3(1), dim3(64), 0, s, e->p, (int)slot, temp, u_tie, d_pi, d_v,
                      d_c);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipMemcpyAsync(pi_o, d_pi, 65 * sizeof(float), hipMemcpyDeviceToHost, s));
@@ -2546,7 +2515,7 @@ int az_make_move(az_engine* e, int32_t slot, int32_t action, void* stream) {
   AZ_REQUIRE(slot >= 0 && slot < e->p.G, AZ_ERR_ARG, "slot out of range");
   AZ_REQUIRE(action >= 0 && action <= 64, AZ_ERR_STATE, "%d", action);
   hipStream_t s = azc::as_stream(stream);
-  hipLaunchKernelGGL(k_reroot, dim3(1), dim3(kMoveBlock), e->lds_move, s, e->dp, (int)slot,
+  hipLaunchKernelGGL(k_reroot, dim3(1), dim3(kMoveBlock), e->lds_move, s, e->p, (int)slot,
                      (int)action, e->d_result);
   AZ_HIP(hipGetLastError());
   int32_t child = -1;
@@ -2573,7 +2542,7 @@ int az_set_roots(az_engine* e, const int32_t* slots, const uint64_t* own, const 
   AZ_HIP(hipMemcpyAsync(e->d_own, own, n * 8, hipMemcpyHostToDevice, s));
   AZ_HIP(hipMemcpyAsync(e->d_opp, opp, n * 8, hipMemcpyHostToDevice, s));
   AZ_HIP(hipMemcpyAsync(e->d_ivec, player, n * 4, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_set_roots, dim3((n + 255) / 256), dim3(256), 0, s, e->dp, e->d_slots,
+  hipLaunchKernelGGL(k_set_roots, dim3((n + 255) / 256), dim3(256), 0, s, e->p, e->d_slots,
                      e->d_own, e->d_opp, e->d_ivec, (int)n);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipStreamSynchronize(s));
@@ -2589,7 +2558,7 @@ int az_begin_search_slots(az_engine* e, const int32_t* slots, int32_t n,
   AZ_REQUIRE(slots, AZ_ERR_ARG, "az_begin_search_slots: null slots");
   hipStream_t s = azc::as_stream(stream);
   AZ_HIP(hipMemcpyAsync(e->d_slots, slots, n * 4, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_begin_slots, dim3((n + 255) / 256), dim3(256), 0, s, e->dp, e->d_slots,
+  hipLaunchKernelGGL(k_begin_slots, dim3((n + 255) / 256), dim3(256), 0, s, e->p, e->d_slots,
                      (int)n, (int)num_simulations);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipStreamSynchronize(s));
@@ -2599,7 +2568,7 @@ int az_begin_search_slots(az_engine* e, const int32_t* slots, int32_t n,
 int az_root_stats(az_engine* e, int32_t* counts, double* vroot, void* stream) {
   AZ_REQUIRE(e && counts, AZ_ERR_ARG, "az_root_stats: null argument");
   hipStream_t s = azc::as_stream(stream);
-  hipLaunchKernelGGL(k_root_stats, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->dp, e->d_counts,
+  hipLaunchKernelGGL(k_root_stats, dim3(sel_grid(e)), dim3(kSelBlock), 0, s, e->p, e->d_counts,
                      e->d_vroot);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipMemcpyAsync(counts, e->d_counts, (size_t)e->p.G * 65 * 4, hipMemcpyDeviceToHost, s));
@@ -2614,7 +2583,7 @@ int az_reroot_slots(az_engine* e, const int32_t* actions, int32_t* found, void* 
   hipStream_t s = azc::as_stream(stream);
   AZ_HIP(hipMemcpyAsync(e->d_ivec, actions, (size_t)e->p.G * 4, hipMemcpyHostToDevice, s));
   const int blocks = e->p.G < 256 ? e->p.G : 256;
-  hipLaunchKernelGGL(k_reroot_slots, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->dp,
+  hipLaunchKernelGGL(k_reroot_slots, dim3(blocks), dim3(kMoveBlock), e->lds_move, s, e->p,
                      e->d_ivec, e->d_found);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipMemcpyAsync(found, e->d_found, (size_t)e->p.G * 4, hipMemcpyDeviceToHost, s));
@@ -2625,7 +2594,7 @@ int az_reroot_slots(az_engine* e, const int32_t* actions, int32_t* found, void* 
 int az_counters(az_engine* e, int64_t* out8, void* stream) {
   AZ_REQUIRE(e && out8, AZ_ERR_ARG, "null argument");
   hipStream_t s = azc::as_stream(stream);
-  hipLaunchKernelGGL(k_sum_sims, dim3(1), dim3(1024), 0, s, e->dp);
+  hipLaunchKernelGGL(k_sum_sims, dim3(1), dim3(1024), 0, s, e->p);
   AZ_HIP(hipGetLastError());
   Counters c;
   AZ_HIP(hipMemcpyAsync(&c, e->p.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));

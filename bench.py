@@ -184,6 +184,31 @@ class _HipEvents:
         self.lib.hipEventDestroy(ev)
 
 
+class _ProfilerWindow:
+    """AZ_PROF_WINDOW=1 under `rocprofv3 --selected-regions`: the profiler records only
+    between roctxProfilerResume and roctxProfilerPause, i.e. the timed window (the warmup's
+    tens of thousands of graph launches are not traced).  A no-op otherwise."""
+
+    def __init__(self):
+        self.lib = None
+        if os.environ.get("AZ_PROF_WINDOW") == "1":
+            import ctypes
+
+            self.lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+            self.lib.roctxProfilerResume.argtypes = [ctypes.c_uint64]
+            self.lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
+
+    def resume(self):
+        if self.lib is not None:
+            torch.cuda.synchronize()
+            self.lib.roctxProfilerResume(0)
+
+    def pause(self):
+        if self.lib is not None:
+            torch.cuda.synchronize()
+            self.lib.roctxProfilerPause(0)
+
+
 def launch_ms(launch, reps, system_fence=False, before=None):
     """Average duration of one launch: a HIP event pair around each launch on its stream
     (the current torch stream, which the entry points are given), so the figure is the
@@ -705,8 +730,10 @@ def main():
         ms_step_kernel = kb.time_ms()
     sp.step(warmup_run)
     barrier()
+    prof = _ProfilerWindow()  # AZ_PROF_WINDOW=1: rocprofv3 --selected-regions traces the window only
     c0 = e.counters()
     t0 = time.perf_counter()
+    prof.resume()
     sp.step(a.steps)
     # per-generation exchange: all-gather the finished games' samples over RCCL/xGMI
     c_mid = e.counters()
@@ -720,6 +747,7 @@ def main():
         allgather_rows = int(sum(counts))
     barrier()
     dt = time.perf_counter() - t0
+    prof.pause()
     c1 = e.counters()
     moves = c1["moves"] - c0["moves"]
     games_done = c1["games_finished"] - c0["games_finished"]
