@@ -595,7 +595,25 @@ class FusedInferenceNet(nn.Module, Inference):
             fuse = (heads_into is not None and not sk and self.fuse_heads
                     and self._fused_heads_ready() and c2s[-1].algo == "wino4"
                     and c2s[-1].precision == "fp16x2" and c2s[-1].channels == 128)
-            t4 = not sk and self._trunk4_ready(c1s, c2s, B)
+            t4 = not sk and self._trunk4_ready(c1s, c2s, B, heads_into_ok=fuse)
+            cap = self._trunk4_cap(c1s[0].wq.device) if c1s else B
+            if t4 and B > cap:
+                # more boards than are resident at once: the persistent trunk per chunk of
+                # `cap` boards (every workgroup of a launch resident, at the same layer),
+                # heads fused (the tower's output is not returned)
+                if not stem_done:
+                    if isinstance(self.stem, _HipStem):
+                        h0 = self.stem(x, absmax=bufs[0])
+                    else:
+                        h0 = self.stem(x)
+                        board_absmax(h0, out=bufs[0])
+                else:
+                    h0 = ent["h0"]
+                for b0 in range(0, B, cap):
+                    b1 = min(B, b0 + cap)
+                    self._trunk4(h0[b0:b1], [bufs[0][b0:b1], bufs[1][b0:b1]], c1s, c2s,
+                                 (heads_into[0][b0:b1], heads_into[1][b0:b1]))
+                return None
             if t4 and not stem_done and isinstance(self.stem, _HipStem):
                 # the stem inside the persistent trunk (each workgroup's boards first)
                 return self._trunk4(None, bufs, c1s, c2s, heads_into if fuse else None, planes=x)
@@ -635,12 +653,21 @@ class FusedInferenceNet(nn.Module, Inference):
     # stem's 33.5 MB store then precedes the first layer instead of hiding under the descents
     trunk_stem = os.environ.get("AZ_TRUNK_STEM", "0") == "1"
 
-    def _trunk4_ready(self, c1s, c2s, B):
+    # AZ_TRUNK4_CHUNKS (default on): batches larger than the resident capacity run the
+    # persistent trunk once per chunk of 4 x CUs boards (with the heads fused), instead of one
+    # launch per layer over the whole batch
+    trunk4_chunks = os.environ.get("AZ_TRUNK4_CHUNKS", "1") != "0"
+
+    def _trunk4_cap(self, dev):
+        """Boards the persistent trunk keeps resident at once: two two-board workgroups per CU."""
+        return 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+
+    def _trunk4_ready(self, c1s, c2s, B, heads_into_ok=False):
         convs = c1s + c2s
         if not (self.fuse_trunk4 and convs and os.environ.get("AZ_W4_BOARDS", "2") == "2"):
             return False
         dev = convs[0].wq.device
-        if B > 4 * torch.cuda.get_device_properties(dev).multi_processor_count:
+        if B > self._trunk4_cap(dev) and not (self.trunk4_chunks and heads_into_ok):
             return False
         if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16x2"
                    and c.channels == 128 for c in convs):
