@@ -54,6 +54,9 @@ constexpr int kMaxLeaves = 8;    // leaves_per_step limit (virtual-loss descents
 #ifndef AZ_SEL_LEVELS
 #define AZ_SEL_LEVELS 14
 #endif
+#ifndef AZ_MOVE_KC
+#define AZ_MOVE_KC 4
+#endif
 #ifndef AZ_ENG_STAMP
 #define AZ_ENG_STAMP 0
 #endif
@@ -1401,7 +1404,7 @@ __device__ int compact(const Params& p, int g, int child, int32_t* scratch, int 
   // 4. copy the members, translating parent / first-child links: kC nodes per thread with
   // every load issued before the first store (one global round trip per kC * block nodes
   // instead of one per block of nodes)
-  constexpr int kC = 4;
+  constexpr int kC = AZ_MOVE_KC;  // 4 (default); experiment builds -DAZ_MOVE_KC=8
   for (int i0 = tid; i0 < n_new; i0 += kMoveBlock * kC) {
     uint64_t own[kC], opp[kC], lg[kC];
     double W[kC], P[kC];
