@@ -94,6 +94,11 @@
 #ifndef AZ_W4_PK
 #define AZ_W4_PK 1
 #endif
+// the lo word of put()'s fp16 split by the mixed-precision FMA (v_fma_mix*_f16); 0 = by
+// conversions and a subtraction (same bits)
+#ifndef AZ_W4_MIX
+#define AZ_W4_MIX AZ_W4_PK
+#endif
 
 namespace {
 
@@ -413,7 +418,7 @@ __device__ __forceinline__ void put(char* slab, f32x2 v, float vsc) {
   if constexpr (G::MODE == AZ_CONV_FP16X2) {
     const f32x2 vs = v * vsc;  // exact: a power of two
     const f16x2 hi = __builtin_convertvector(vs, f16x2);
-#if AZ_W4_PK
+#if AZ_W4_MIX
     // lo = RN16(vs - hi) per element by the mixed-precision FMA (hi read as f16, vs - hi
     // exact in f32, rounded once to f16): two v_fma_mix*_f16 instead of two f16 -> f32
     // conversions, the subtraction and a second packed conversion; bit-identical
