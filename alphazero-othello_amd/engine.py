@@ -435,6 +435,12 @@ class BatchedSelfPlay:
 
     @torch.no_grad()
     def step(self, n=1):
+        self._advance(n)
+        if n > 0:
+            self._flush()
+
+    def _advance(self, n):
+        """n simulation steps on the current stream, without the closing flush."""
         if self.use_graph and self.graph is None:
             try:
                 self._capture()
@@ -463,12 +469,22 @@ class BatchedSelfPlay:
                     left -= 1
                     if self.defer_moves:
                         self._par ^= 1
-        if self.defer_moves and n > 0:
+
+    def _flush(self):
+        if self.defer_moves:
             # the last step's leaves (fused expansion) and moves, so results read after step()
             # returns are complete
             if self.fuse_expand:
                 self.engine.expand_par(self._par ^ 1)
             self.engine.move_flush(self._par ^ 1)
+
+    def counters(self):
+        return self.engine.counters()
+
+    def samples_since(self, c0, device=False):
+        """Sample rows recorded since counters() returned c0."""
+        n = self.counters()["samples"] - c0["samples"]
+        return self.engine.samples(c0["samples"], n, device=device)
 
     def play_games(self, n_games, max_steps=None, check_every=256):
         """Play exactly n_games complete games (slots restart until the budget is used);
@@ -484,6 +500,92 @@ class BatchedSelfPlay:
             done = e.counters()["games_finished"]
         check_complete(e.counters(), n_games)
         return samples_to_tuples(e.samples())
+
+
+class PipelinedSelfPlay:
+    """G concurrent self-play games as P independent BatchedSelfPlay pipelines of G / P slots,
+    each replaying its own HIP graphs on its own HIP stream.  A pipeline's step is three
+    dependent launches (select + expansion + moves, the trunk, the heads-fused conv); the
+    select launch leaves most of the chip idle while its slowest descents finish (DESIGN.md
+    §5), and with two pipelines the other one's trunk fills it.  Per pipeline nothing changes
+    (same kernels and games as a BatchedSelfPlay of G / P slots with its seed and stream id:
+    tests/test_pipelined_gpu.py); the host enqueues `steps_per_graph` steps of each pipeline in
+    turn.  Pipeline i draws Philox stream stream_id * P + i; its sample rows' slot ids are
+    offset by i * G / P."""
+
+    def __init__(self, net, args, n_games, pipelines=2, seed=0, stream_id=0, **kw):
+        if pipelines < 1 or n_games % pipelines:
+            raise ValueError(f"{n_games} games do not split into {pipelines} pipelines")
+        self.P, self.G = int(pipelines), int(n_games)
+        self.parts = [BatchedSelfPlay(net, args, n_games // pipelines, seed=seed,
+                                      stream_id=stream_id * pipelines + i, **kw)
+                      for i in range(pipelines)]
+        p0 = self.parts[0]
+        self.device = p0.device
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.parts]
+        self.args, self.net = p0.args, p0.net
+        self.defer_moves, self.engine_stem = p0.defer_moves, p0.engine_stem
+
+    @property
+    def graph(self):
+        return self.parts[0].graph
+
+    @property
+    def graph_error(self):
+        return next((p.graph_error for p in self.parts if p.graph_error), None)
+
+    def reset(self, start_budget=-1, stagger_steps=0):
+        for i, p in enumerate(self.parts):
+            b = -1 if start_budget < 0 else start_budget // self.P + (i < start_budget % self.P)
+            p.reset(b, stagger_steps)
+
+    @torch.no_grad()
+    def step(self, n=1):
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)
+        k = max(p.steps_per_graph for p in self.parts)
+        left = n
+        while left > 0:  # round-robin, k steps of each pipeline at a time
+            m = min(k, left)
+            for p, s in zip(self.parts, self.streams):
+                with torch.cuda.stream(s):
+                    p._advance(m)
+            left -= m
+        if n > 0:
+            for p, s in zip(self.parts, self.streams):
+                with torch.cuda.stream(s):
+                    p._flush()
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def counters(self):
+        per = [p.counters() for p in self.parts]
+        out = {k: sum(c[k] for c in per) for k in per[0]}
+        out["per_part"] = per
+        return out
+
+    def samples_since(self, c0, device=False):
+        rows = [p.samples_since(c, device=device) for p, c in zip(self.parts, c0["per_part"])]
+        cat = (lambda xs: torch.cat(xs)) if device else (lambda xs: np.concatenate(xs))
+        for i, r in enumerate(rows):
+            r["slot"] = r["slot"] + i * (self.G // self.P)
+        return {k: cat([r[k] for r in rows]) for k in rows[0]}
+
+    def play_games(self, n_games, max_steps=None, check_every=256):
+        """Play exactly n_games complete games over the pipelines; returns the reference's
+        training tuples of every game."""
+        self.reset(start_budget=n_games)
+        c0 = {"samples": 0, "per_part": [{"samples": 0} for _ in self.parts]}
+        G = self.G // self.P
+        limit = max_steps or (n_games // max(1, G) + 2) * 200 * (self.args["num_simulations"] + 2)
+        steps = 0
+        while self.counters()["games_finished"] < n_games and steps < limit:
+            self.step(check_every)
+            steps += check_every
+        for i, p in enumerate(self.parts):
+            check_complete(p.counters(), n_games // self.P + (i < n_games % self.P))
+        return samples_to_tuples(self.samples_since(c0))
 
 
 def check_complete(c, n_games):

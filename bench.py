@@ -120,6 +120,10 @@ def parse():
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="simulation steps captured per HIP graph (rocprofv3's kernel tracer "
                          "records 8-step graphs completely: DESIGN.md section 5)")
+    ap.add_argument("--pipelines", type=int, default=None,
+                    help="the GPU's games as this many independent pipelines, each on its own "
+                         "HIP stream (engine.PipelinedSelfPlay: one pipeline's select launch "
+                         "overlaps another's trunk); default 2 for c3, 1 otherwise")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=None,
@@ -138,6 +142,8 @@ def parse():
     a.net = a.net or preset[2]
     a.d4, a.precision = preset[3], preset[4]
     a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "fp16x2")
+    if a.pipelines is None:
+        a.pipelines = 2 if a.workload == "c3" and a.games % 2 == 0 else 1
     return a
 
 
@@ -693,19 +699,20 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=device)
 
-    from engine import BatchedSelfPlay
+    from engine import BatchedSelfPlay, PipelinedSelfPlay
 
     net = make_net(a.net)
     args = dict(SELFPLAY_ARGS, num_simulations=a.sims)
-    sp = BatchedSelfPlay(net, args, a.games, seed=1234, stream_id=rank,
-                         use_graph=not a.no_graph, require_graph=not a.no_graph,
-                         device=device, d4_augment=a.d4,
-                         dtype=torch.float16 if a.precision == "fp16" else torch.float32,
-                         sample_capacity=a.games * 130 * 4, steps_per_graph=a.steps_per_graph,
-                         defer_moves=not a.no_defer,
-                         engine_stem=not a.no_engine_stem,
-                         precision=a.conv_precision, leaves_per_step=a.leaves)
-    e = sp.engine
+    kw = dict(seed=1234, stream_id=rank, use_graph=not a.no_graph, require_graph=not a.no_graph,
+              device=device, d4_augment=a.d4,
+              dtype=torch.float16 if a.precision == "fp16" else torch.float32,
+              sample_capacity=a.games // a.pipelines * 130 * 4, steps_per_graph=a.steps_per_graph,
+              defer_moves=not a.no_defer, engine_stem=not a.no_engine_stem,
+              precision=a.conv_precision, leaves_per_step=a.leaves)
+    if a.pipelines > 1:
+        sp = PipelinedSelfPlay(net, args, a.games, pipelines=a.pipelines, **kw)
+    else:
+        sp = BatchedSelfPlay(net, args, a.games, **kw)
     if os.environ.get("AZ_DUMP_MAPS"):  # diagnostics: the address map, to place a fault's PC
         with open("/proc/self/maps") as f_in, open(os.environ["AZ_DUMP_MAPS"], "w") as f_out:
             f_out.write(f_in.read())
@@ -731,24 +738,23 @@ def main():
     sp.step(warmup_run)
     barrier()
     prof = _ProfilerWindow()  # AZ_PROF_WINDOW=1: rocprofv3 --selected-regions traces the window only
-    c0 = e.counters()
+    c0 = sp.counters()
     t0 = time.perf_counter()
     prof.resume()
     sp.step(a.steps)
     # per-generation exchange: all-gather the finished games' samples over RCCL/xGMI
-    c_mid = e.counters()
+    c_mid = sp.counters()
     n_new = c_mid["samples"] - c0["samples"]
     allgather_rows = n_new
     if dist is not None:
         from dist_replay import allgather_samples
 
-        pooled, counts = allgather_samples(e.samples(c0["samples"], n_new, device=not rehearse),
-                                           coll_device)
+        pooled, counts = allgather_samples(sp.samples_since(c0, device=not rehearse), coll_device)
         allgather_rows = int(sum(counts))
     barrier()
     dt = time.perf_counter() - t0
     prof.pause()
-    c1 = e.counters()
+    c1 = sp.counters()
     moves = c1["moves"] - c0["moves"]
     games_done = c1["games_finished"] - c0["games_finished"]
     sims = c1["simulations"] - c0["simulations"]
@@ -784,6 +790,7 @@ def main():
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
                    "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
+                   "pipelines": a.pipelines,
                    "hip_graph": sp.graph is not None, "graph_error": sp.graph_error,
                    "deferred_moves": sp.defer_moves, "engine_stem": sp.engine_stem},
         "value_basis": basis,
