@@ -572,9 +572,9 @@ class PipelinedSelfPlay:
             r["slot"] = r["slot"] + i * (self.G // self.P)
         return {k: cat([r[k] for r in rows]) for k in rows[0]}
 
-    def play_games(self, n_games, max_steps=None, check_every=256):
+    def play_games(self, n_games, max_steps=None, check_every=256, tuples=True):
         """Play exactly n_games complete games over the pipelines; returns the reference's
-        training tuples of every game."""
+        training tuples of every game (tuples=False: the sample rows)."""
         self.reset(start_budget=n_games)
         c0 = {"samples": 0, "per_part": [{"samples": 0} for _ in self.parts]}
         G = self.G // self.P
@@ -585,7 +585,8 @@ class PipelinedSelfPlay:
             steps += check_every
         for i, p in enumerate(self.parts):
             check_complete(p.counters(), n_games // self.P + (i < n_games % self.P))
-        return samples_to_tuples(self.samples_since(c0))
+        rows = self.samples_since(c0)
+        return samples_to_tuples(rows) if tuples else rows
 
 
 def check_complete(c, n_games):

@@ -68,7 +68,7 @@ def one_self_play(args_tuple):
 
 def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, stream_id=0,
                             d4_augment=False, dtype=torch.float32, group=None,
-                            sync_weights=True):
+                            sync_weights=True, pipelines=1):
     """Batched replacement of Trainer.collect_self_play_games' pool (train.py:199-225):
     `num_games` games on the GPU, `n_slots` at a time (default min(games, 4096)), each
     searching with args['num_threads'] virtual-loss leaves per step (the reference's worker
@@ -81,13 +81,18 @@ def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, strea
     0 (`sync_weights`; the reference hands every pool worker the best net's state_dict,
     train.py:205-207), and ONE all-gather (dist_replay.allgather_samples: RCCL over xGMI
     with the "nccl" backend) pools every rank's rows on every rank -- each rank returns the
-    same list, rank 0's games first."""
+    same list, rank 0's games first.
+
+    pipelines > 1: the rank's slots as that many independent pipelines on their own HIP
+    streams (engine.PipelinedSelfPlay; +8-10 % on configs[1] / configs[4]-sized batches,
+    profiles/r04_pipelines_ab.json)."""
     import torch.distributed as dist
 
     distributed = dist.is_available() and dist.is_initialized() and \
         dist.get_world_size(group) > 1
     if not distributed:
-        rows = _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype)
+        rows = _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype,
+                           pipelines)
         return _rows_to_tuples(rows)
     from dist_replay import allgather_samples, broadcast_state_dict
 
@@ -98,7 +103,8 @@ def collect_self_play_games(policy, args, num_games, n_slots=None, seed=0, strea
         broadcast_state_dict(policy.to(dev), src=0, group=group)
         policy.to(home)
     mine = num_games // world + (1 if rank < num_games % world else 0)
-    rows = _local_rows(policy, args, mine, n_slots, seed, stream_id + rank, d4_augment, dtype)
+    rows = _local_rows(policy, args, mine, n_slots, seed, stream_id + rank, d4_augment, dtype,
+                       pipelines)
     pooled, _ = allgather_samples(rows, dev, group=group)
     return _rows_to_tuples({k: v.cpu().numpy() for k, v in pooled.items()})
 
@@ -112,20 +118,25 @@ def _collective_device(group=None):
     return torch.device("cpu")
 
 
-def _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype):
+def _local_rows(policy, args, num_games, n_slots, seed, stream_id, d4_augment, dtype,
+                pipelines=1):
     """This process's games as engine sample rows (numpy: own/opp canonical bitboards, pi,
     z, player); none when num_games is 0."""
     if num_games <= 0:
         return {"own": np.zeros(0, np.uint64), "opp": np.zeros(0, np.uint64),
                 "pi": np.zeros((0, 65), np.float32), "z": np.zeros(0, np.float64),
                 "player": np.zeros(0, np.int8)}
-    from engine import BatchedSelfPlay
+    from engine import BatchedSelfPlay, PipelinedSelfPlay
 
     n_slots = n_slots or min(num_games, 4096)
-    sp = BatchedSelfPlay(policy, args, n_slots, seed=seed, stream_id=stream_id,
-                         d4_augment=d4_augment, dtype=dtype,
-                         sample_capacity=num_games * 130,
-                         leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
+    kw = dict(seed=seed, stream_id=stream_id, d4_augment=d4_augment, dtype=dtype,
+              sample_capacity=num_games * 130,
+              leaves_per_step=min(8, max(1, int(args.get("num_threads", 4)))))
+    if pipelines > 1 and n_slots >= pipelines:
+        n_slots -= n_slots % pipelines
+        sp = PipelinedSelfPlay(policy, args, n_slots, pipelines=pipelines, **kw)
+        return sp.play_games(num_games, tuples=False)
+    sp = BatchedSelfPlay(policy, args, n_slots, **kw)
     sp.play_games(num_games)
     return sp.engine.samples()
 

@@ -123,7 +123,8 @@ def parse():
     ap.add_argument("--pipelines", type=int, default=None,
                     help="the GPU's games as this many independent pipelines, each on its own "
                          "HIP stream (engine.PipelinedSelfPlay: one pipeline's select launch "
-                         "overlaps another's trunk); default 2 for c3, 1 otherwise")
+                         "overlaps another's trunk); default 2 for c2 and c5 (measured +8 / "
+                         "+10 %%), 1 for c3 and c4 (no gain / -4.5 %%: profiles/r04_pipelines_ab.json)")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=None,
@@ -143,7 +144,7 @@ def parse():
     a.d4, a.precision = preset[3], preset[4]
     a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "fp16x2")
     if a.pipelines is None:
-        a.pipelines = 2 if a.workload == "c3" and a.games % 2 == 0 else 1
+        a.pipelines = 2 if a.workload in ("c2", "c5") and a.games % 2 == 0 else 1
     return a
 
 

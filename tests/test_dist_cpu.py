@@ -162,7 +162,7 @@ def _collect_worker(rank, world, port, q, num_games):
 
     calls = []
 
-    def fake_local_rows(policy, args, n, n_slots, seed, stream_id, d4, dtype):
+    def fake_local_rows(policy, args, n, n_slots, seed, stream_id, d4, dtype, pipelines=1):
         calls.append((n, stream_id, float(policy.fc_value2.weight.sum())))
         return _rows(100 * rank + stream_id, 7 * n)
 

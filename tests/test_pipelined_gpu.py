@@ -26,13 +26,18 @@ def _sorted(s):
 def _net(kind):
     if kind == "mock":
         return MockNet(), {"fold": False}
-    from Models import AlphaZeroNet
+    from Models import AlphaZeroNet, FastOthelloNet
 
-    torch.manual_seed(0)  # the bench's net: fp16x2 persistent trunk + heads-fused conv
-    return AlphaZeroNet(8, 65, 5, 128), {}
+    torch.manual_seed(0)
+    if kind == "fast":  # configs[1]'s net (bench --workload c2: 2 pipelines by default)
+        return FastOthelloNet(8, 65), {}
+    if kind == "c5":  # configs[4]: fused D4 symmetry + fp16 inference (2 pipelines by default)
+        return AlphaZeroNet(8, 65, 5, 128), {"d4_augment": True, "dtype": torch.float16}
+    return AlphaZeroNet(8, 65, 5, 128), {}  # fp16x2 persistent trunk + heads-fused conv
 
 
-@pytest.mark.parametrize("use_graph,kind", [(True, "mock"), (False, "mock"), (True, "az5x128")])
+@pytest.mark.parametrize("use_graph,kind", [(True, "mock"), (False, "mock"), (True, "az5x128"),
+                                            (True, "fast"), (True, "c5")])
 def test_pipelines_play_the_standalone_games(use_graph, kind):
     G, P, steps = 512, 2, 1300
     net, extra = _net(kind)

@@ -254,8 +254,8 @@ def test_batched_selfplay_with_virtual_loss_properties():
     assert (np.abs(smp["z"]) <= 1.0).all()
 
 
-@pytest.mark.parametrize("threads", [None, 1])
-def test_collect_self_play_games_drop_in(threads):
+@pytest.mark.parametrize("threads,pipelines", [(None, 1), (1, 1), (1, 2)])
+def test_collect_self_play_games_drop_in(threads, pipelines):
     """self_play_worker.collect_self_play_games (the batched replacement of train.py's pool)
     at the reference's default worker count (4 leaves per step) and at num_threads = 1:
     the reference's training tuples, one list per call."""
@@ -270,7 +270,7 @@ def test_collect_self_play_games_drop_in(threads):
             "lambda": 0.98}
     if threads is not None:
         args["num_threads"] = threads
-    out = collect_self_play_games(FastOthelloNet(8, 65), args, 20)
+    out = collect_self_play_games(FastOthelloNet(8, 65), args, 20, pipelines=pipelines)
     assert len(out) >= 9 * 20
     for s, pi, z in out:
         assert s.shape == (8, 8) and s.dtype == np.int8
