@@ -118,6 +118,26 @@ __device__ unsigned long long g_w4_stamps[1024 * 16];
   do {              \
   } while (0)
 #endif
+// experiment builds only (-DAZ_W4_TSTAMP=1, scripts/trunk_stamps.py): the persistent trunk's
+// per-layer timeline, workgroup wave 0's s_memtime at each conv's start (after the layer
+// fence), after its prologue, before its first epilogue, and at its end, [wg < 1024][layer <
+// 16][4], lane 0's vector store
+#ifndef AZ_W4_TSTAMP
+#define AZ_W4_TSTAMP 0
+#endif
+#if AZ_W4_TSTAMP
+__device__ unsigned long long g_w4_tst[1024 * 16 * 4];
+#define W4T_STAMP(layer, i)                                                              \
+  do {                                                                                   \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && (layer) < 16)                           \
+      g_w4_tst[(blockIdx.x * 16 + (layer)) * 4 + (i)] = t_;                              \
+  } while (0)
+#else
+#define W4T_STAMP(layer, i) \
+  do {                      \
+  } while (0)
+#endif
 // experiment builds only (-DAZ_W4_CSTAMP=1, scripts/w4_chunk_stamps.py): every wave's
 // s_memtime at each chunk's start, before and after its closing barrier, [wg < 256][wave]
 // [chunk][3], lane 0's vector store
@@ -857,10 +877,12 @@ template <class G, bool RES, bool RELU, bool HEADS = false, bool LAUNDER = false
 __device__ __forceinline__ void conv_body(
     const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
-    float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho) {
+    float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho,
+    int layer = 0) {
   constexpr int C = G::C;
   extern __shared__ float4 lds4[];
   W4_STAMP(0);
+  W4T_STAMP(layer, 0);
   St<G> S;
   S.lds = reinterpret_cast<char*>(lds4);
   S.x = x;
@@ -999,6 +1021,7 @@ __device__ __forceinline__ void conv_body(
     }
   }
   W4_STAMP(1);
+  W4T_STAMP(layer, 1);
   if (AZ_W4_PRIO == 1 && G::WAVES == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
     __builtin_amdgcn_s_setprio(1);
   if constexpr (G::NG == 1) {  // one transform row: its partial outputs, both halves
@@ -1029,6 +1052,7 @@ __device__ __forceinline__ void conv_body(
   constexpr bool STAGED = RES && G::RES_FITS && !G::SPLIT;
   run_group<G, 2, STAGED ? 0 : -1>(S);
   W4_STAMP(4);
+  W4T_STAMP(layer, 2);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
   epilogue<G, 0, RES, RELU, HEADS>(S, E, res, y, rt0, h);
   if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
@@ -1057,6 +1081,7 @@ __device__ __forceinline__ void conv_body(
   // read its entries in the prologue, before the first barrier)
   if (G::SCALED && !G::SPLIT && tid < G::BOARDS && tid < nb) in_absmax[b0 + tid] = 0.0f;
   W4_STAMP(6);
+  W4T_STAMP(layer, 3);
   }
 }
 
@@ -1220,7 +1245,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
     if ((i & 1) == 0) {
       conv_body<G, false, true, false, true>(h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]),
                                              nullptr, a.t, a.n_boards,
-                                             a.amax[0], a.amax[1], HeadsOut{});
+                                             a.amax[0], a.amax[1], HeadsOut{}, i);
     } else {
       // the last layer of a HEADS launch keeps no range (nothing reads its output as a
       // conv input): amax[0] stays as the stem / caller left it
@@ -1228,7 +1253,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
       conv_body<G, true, true, false, true>(a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h,
                                             a.hb[ob], a.n_boards,
                                             a.amax[1], last_heads ? nullptr : a.amax[0],
-                                            HeadsOut{});
+                                            HeadsOut{}, i);
       h = a.hb[ob];
       ob ^= 1;
     }
@@ -1386,6 +1411,13 @@ extern "C" int az_conv3x3_wino4_splitk_gpu(const float* x, const void* wq, const
                         "az_conv3x3_wino4_splitk_gpu: splits must be 2, 4, 8, 16 or 32, got %d",
                         splits);
 }
+
+#if AZ_W4_TSTAMP
+extern "C" int az_w4_tstamps(unsigned long long* host, int n) {
+  AZ_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w4_tst), sizeof(unsigned long long) * n));
+  return AZ_OK;
+}
+#endif
 
 #if AZ_W4_CSTAMP
 extern "C" int az_w4_cstamps(unsigned long long* host, int n) {
