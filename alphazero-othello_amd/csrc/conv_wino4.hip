@@ -99,6 +99,12 @@
 #ifndef AZ_W4_MIX
 #define AZ_W4_MIX AZ_W4_PK
 #endif
+// the layer's last two chunks skip the pipeline's look-ahead past the end (clamped duplicates:
+// input slices, their LDS stores and window reads, the last chunk's weight steps, transform
+// and A fragments) -- none of it was ever used
+#ifndef AZ_W4_TAIL
+#define AZ_W4_TAIL 0
+#endif
 
 namespace {
 
@@ -607,9 +613,12 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // KR / KS: the transform-grid rows of chunks v+1 (whose rows are combined here) and v+2
 // (whose windows are read at the end), when known at compile time (AZ_W4_DIET); -1 = from
 // the chunk map at run time
-template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false>
+// TAIL (AZ_W4_TAIL): 1 = the layer's second-to-last chunk (its input-slice look-ahead is past
+// the end), 2 = the last (everything after its own MFMAs is)
+template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false, int TAIL = 0>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
+  constexpr bool NO_IN = TAIL >= 1, NO_NEXT = TAIL == 2;
   W4C_STAMP(v, 0);
   const int L = lmap<G>(S, v);
   const char* cur = S.lds + (v & 1) * G::BUF;
@@ -623,7 +632,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
 #pragma unroll
   for (int l = 0; l < 4; ++l) {
     Frag<G> an[G::NRT];
-    if (l < 3 && !(AZ_W4_EXP & 16)) read_a<G>(an, cur, l + 1, S.aoff);
+    if (l < 3 && !(AZ_W4_EXP & 16)) read_a<G>(an, cur, l + 1, S.aoff);  // this chunk's: kept
     if (l < 3 && (AZ_W4_EXP & 16)) {
 #pragma unroll
       for (int t = 0; t < G::NRT; ++t) an[t] = S.af[t];
@@ -635,7 +644,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
       for (int t = 0; t < G::NRT; ++t) mma<G, FIRST>(S.acc[l][t], S.af[t], S.bf[slot]);
       if (AZ_W4_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
-    if (l == 0 && !(AZ_W4_EXP & 2)) {
+    if (l == 0 && !(AZ_W4_EXP & 2) && !NO_NEXT) {
       // chunk L+1's window rows (requested right after the previous barrier) combined
       // behind step 0's MFMAs
 #pragma unroll
@@ -646,7 +655,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
           combine_rows(S.rk[u], S.dr[u], Lr);
       }
     }
-    if (!(AZ_W4_EXP & 1) && (!(AZ_W4_EXP & 32) || S.tid < 256)) {
+    if (!(AZ_W4_EXP & 1) && (!(AZ_W4_EXP & 32) || S.tid < 256) && !(NO_NEXT && l + G::PD >= 4)) {
       if constexpr (AZ_W4_DIET)
         load_b<G>(S.bf[(slot + G::PD) % G::RING], S.rw, S.wlane, qmap<G>(S, v * 4 + l + G::PD));
       else
@@ -654,7 +663,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     }
     // the chunk-after-next's input slice at the chunk's first step: four steps of latency
     // cover before it is stored to LDS at the chunk's end
-    if (l == 0 && !(AZ_W4_EXP & 2)) {
+    if (l == 0 && !(AZ_W4_EXP & 2) && !NO_IN) {
       if constexpr (AZ_W4_DIET)
         load_in<G>(S.ld[set_l], S.rx, S.goff, Ll);
       else
@@ -664,7 +673,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
       if (l == 1) res_dma<G, STAGE>(S, L & 7);
     }
 #pragma unroll
-    for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
+    for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2) && !NO_NEXT; ++u) {
       const float vs = CT ? 1.0f : S.vsc[u];  // CT: the scale is in rk already
       if (l == 0) put_point<G, 0>(nxt, S.rk[u], S.soff[u], vs);
       if (l == 1) put_point<G, 1>(nxt, S.rk[u], S.soff[u], vs);
@@ -690,14 +699,14 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     __builtin_amdgcn_sched_barrier(0);
   }
   // slot (v+2) & 1 = v & 1 held chunk v's input, whose rows were formed in chunk v-1
-  if (!(AZ_W4_EXP & 2)) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
+  if (!(AZ_W4_EXP & 2) && !NO_IN) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
   W4C_STAMP(v, 1);
   if (!(AZ_W4_EXP & 8)) lds_barrier();
   W4C_STAMP(v, 2);
-  read_a<G>(S.af, nxt, 0, S.aoff);
+  if (!NO_NEXT) read_a<G>(S.af, nxt, 0, S.aoff);
   // the next chunk's window rows (chunk L+2, stored just before the barrier)
 #pragma unroll
-  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2); ++u) {
+  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2) && !NO_IN; ++u) {
     if constexpr (CT)
       read_rows_k<G, KS < 4 ? KS : 3, PAR>(S.dr[u], S.lds, S.cbase[u]);
     else
@@ -746,8 +755,9 @@ __device__ __forceinline__ void run_group(St<G>& S) {
       run_chunk<G, 0, STAGE, K, K>(S, KV * G::NC + c);
       run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + c + 1);
     }
-    run_chunk<G, 0, STAGE, K, KN>(S, KV * G::NC + G::NC - 2);
-    run_chunk<G, 1, STAGE, KN, KN>(S, KV * G::NC + G::NC - 1);
+    constexpr int T1 = AZ_W4_TAIL && K == 3 ? 1 : 0, T2 = AZ_W4_TAIL && K == 3 ? 2 : 0;
+    run_chunk<G, 0, STAGE, K, KN, false, T1>(S, KV * G::NC + G::NC - 2);
+    run_chunk<G, 1, STAGE, KN, KN, false, T2>(S, KV * G::NC + G::NC - 1);
   } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
     constexpr int KN = K + 1;
 #pragma unroll 1
