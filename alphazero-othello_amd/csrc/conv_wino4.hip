@@ -967,10 +967,14 @@ __device__ __forceinline__ void conv_body(
 
   // ---- prologue: zero both input slots (their borders stay zero), chunk 0 and 1 slices and
   // the first weight steps in flight together; chunk 0 transformed into V buffer 0
+  // (the persistent trunk's later layers: the borders are still zero -- interior stores never
+  // touch them -- and the layer fence ordered the previous layer's reads)
+  const bool fill = !LAUNDER || layer == 0;
   {
     char* in0 = S.lds + G::IN_OFF;
-    for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
-      *reinterpret_cast<f32x4*>(in0 + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (fill)
+      for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
+        *reinterpret_cast<f32x4*>(in0 + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 ld0[G::LD_PER_THREAD], ld1[G::LD_PER_THREAD];
     if constexpr (AZ_W4_DIET) {
       load_in<G>(ld0, S.rx, S.goff, lmap<G>(S, 0));
@@ -985,7 +989,7 @@ __device__ __forceinline__ void conv_body(
 #pragma unroll
       for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], wq, S.wlane, qmap<G>(S, i));
     }
-    lds_barrier();  // the zero fill before any interior store
+    if (fill) lds_barrier();  // the zero fill before any interior store
     store_in<G>(in0, ld0, S.ldst);
     store_in<G>(in0 + G::IN_SLOT, G::IPD == 1 ? S.ld[0] : ld1, S.ldst);
     if (G::IPD == 1) {  // stored at the end of chunk 0
