@@ -1234,9 +1234,16 @@ __device__ __forceinline__ void trunk_heads(const float* __restrict__ y, int n_b
 // the tower and the heads in one launch, no kernel boundary before the last layer.  (The
 // heads in the last conv's epilogue, inlined here as a third body, spilled ~100 VGPRs into
 // the layer loop.)
+// AZ_W4_TRUNK_HEADS_EPI (HEADS launches): 1 = the last conv runs after the layer loop as the
+// heads-fused body (heads from the accumulators, as az_conv3x3_wino4_heads_gpu; no store and
+// read-back of the tower's output); 0 = the last conv in the loop, then trunk_heads
+#ifndef AZ_W4_TRUNK_HEADS_EPI
+#define AZ_W4_TRUNK_HEADS_EPI 0
+#endif
 template <class G, bool HEADS = false>
 __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a,
                                                                       HeadsOut ho) {
+  constexpr bool EPI = HEADS && AZ_W4_TRUNK_HEADS_EPI;
 #if AZ_W4_STAGGER
   // experiment: the second half of the grid (the second workgroup on each CU when every
   // workgroup is resident) starts later, so the two co-resident workgroups' phases differ
@@ -1255,7 +1262,8 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   }
   const float* h = a.h_in;
   int ob = 0;
-  for (int i = 0; i < a.n_convs; ++i) {
+  const int n_loop = EPI ? a.n_convs - 1 : a.n_convs;
+  for (int i = 0; i < n_loop; ++i) {
     if (i > 0) layer_fence();
     if ((i & 1) == 0) {
       conv_body<G, false, true, false, true>(h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]),
@@ -1273,7 +1281,12 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
       ob ^= 1;
     }
   }
-  if constexpr (HEADS) {
+  if constexpr (EPI) {
+    layer_fence();  // the last block's first conv output (t) visible to this workgroup
+    const int i = a.n_convs - 1;
+    conv_body<G, true, true, true, true>(a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h,
+                                         nullptr, a.n_boards, a.amax[1], nullptr, ho, i);
+  } else if constexpr (HEADS) {
     layer_fence();  // the last layer's stores drained and visible to this workgroup's reads
     trunk_heads<G>(h, a.n_boards, ho);
   }
