@@ -711,12 +711,14 @@ class FusedInferenceNet(nn.Module, Inference):
             return None
         return h_last
 
-    # AZ_TRUNK_HEADS=1: the heads inside the persistent trunk's launch, after its last conv
-    # (az_trunk_wino4_heads_gpu, bit-identical) instead of the heads-fused last conv as a
-    # launch of its own.  Off: B = 1,024 evaluation 449-451 vs 445-446 us, configs[2] bench
-    # 96.6-96.8 vs 97.6 games/s same box (profiles/r04_net_ab.json) -- the last layer's output
-    # then makes an L2 round trip the fused epilogue avoids
-    trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "0") == "1"
+    # AZ_TRUNK_HEADS (default on): the heads inside the persistent trunk's launch
+    # (az_trunk_wino4_heads_gpu, bit-identical), its last conv run after the layer loop as the
+    # heads-fused body, instead of the heads-fused last conv as a launch of its own: B = 1,024
+    # evaluation 423.3 vs 424.6 us, configs[2] 102.8-102.9 vs 102.5-102.7 games/s same box
+    # (profiles/r04_trunk_heads_epi_ab.json).  (Its first form stored the last layer's output
+    # and read it back for the heads: 4 us slower, profiles/r04_net_ab.json.)  AZ_TRUNK_HEADS=0:
+    # the separate heads-fused conv launch
+    trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "1") == "1"
 
     def _trunk4_heads(self, h, bufs, c1s, heads_into, planes=None):
         """The whole tower and the heads in one az_trunk_wino4_heads_gpu launch."""

@@ -1236,9 +1236,12 @@ __device__ __forceinline__ void trunk_heads(const float* __restrict__ y, int n_b
 // the layer loop.)
 // AZ_W4_TRUNK_HEADS_EPI (HEADS launches): 1 = the last conv runs after the layer loop as the
 // heads-fused body (heads from the accumulators, as az_conv3x3_wino4_heads_gpu; no store and
-// read-back of the tower's output); 0 = the last conv in the loop, then trunk_heads
+// read-back of the tower's output; 242 VGPRs, no spills): B = 1,024 evaluation 423.3 vs 424.6
+// us for the tower launch + heads-fused conv launch and 431.4 for the read-back form, bench
+// +0.2 %, bit-identical (profiles/r04_trunk_heads_epi_ab.json); 0 = the last conv in the loop,
+// then trunk_heads (the read-back form)
 #ifndef AZ_W4_TRUNK_HEADS_EPI
-#define AZ_W4_TRUNK_HEADS_EPI 0
+#define AZ_W4_TRUNK_HEADS_EPI 1
 #endif
 template <class G, bool HEADS = false>
 __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 a,
