@@ -2,15 +2,20 @@
 driver loop that replaces the reference's process-pool of `one_self_play` calls
 (train.py:199-225, self_play_worker.py:38-88).
 
-Per simulation step (all on one HIP stream, no host synchronisation, optionally one
-captured HIP graph):
+Per simulation step (all on one HIP stream, no host synchronisation, replayed from HIP
+graphs of 8 steps).  The plain sequence (Engine's host-driven API, the drop-in MCTS):
 
     az_select         leaves of every active game -> canonical planes nn_in [G*K, 64]
                       (K = leaves_per_step: virtual-loss descents per game per step)
-    net               PyTorch-ROCm forward on nn_in -> softmax priors [G, 65], values [G]
-    az_expand_backup  eager expansion + backup
+    net               the leaf evaluation on nn_in -> priors [G*K, 65], values [G*K]
+    az_expand_backup  expansion + backup
     az_play           games whose search finished: pi, record, sample, move, TD(lambda)
                       targets on game end, re-root; finished slots restart
+
+BatchedSelfPlay's default merges them into two launches per step: az_select_move_expand
+(the previous step's expansions, the descents, the previous step's moves and the net's stem,
+one wave per game) and the net (Models.FusedInferenceNet: the persistent HIP trunk with the
+policy / value heads in its last conv).
 
 The host only reads counters.  Finished games' samples accumulate in a device buffer in
 the reference's training-tuple layout (canonical state, pi, target).
@@ -504,8 +509,8 @@ class BatchedSelfPlay:
 
 class PipelinedSelfPlay:
     """G concurrent self-play games as P independent BatchedSelfPlay pipelines of G / P slots,
-    each replaying its own HIP graphs on its own HIP stream.  A pipeline's step is three
-    dependent launches (select + expansion + moves, the trunk, the heads-fused conv); the
+    each replaying its own HIP graphs on its own HIP stream.  A pipeline's step is dependent
+    launches (select + expansion + moves, then the net: the persistent trunk with the heads); the
     select launch leaves most of the chip idle while its slowest descents finish (DESIGN.md
     §5), and with two pipelines the other one's trunk fills it.  Per pipeline nothing changes
     (same kernels and games as a BatchedSelfPlay of G / P slots with its seed and stream id:
