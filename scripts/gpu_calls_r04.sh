@@ -442,7 +442,24 @@ c22() {
   exit 0
 }
 
+c23() {
+  # round 4, final library: the default bench line twice more and the configs[1] / configs[4]
+  # lines (two pipelines), for the spread on one more box
+  set -u
+  export OUT=gpurun_out/r04w TMPDIR=/tmp
+  mkdir -p $OUT
+  for r in 1 2; do
+    timeout -k 10 400 python bench.py --skip-cpu > $OUT/bench_$r.log 2>&1 || exit 1
+    echo "c3 $(tail -1 $OUT/bench_$r.log | cut -c1-120)"
+  done
+  for w in c5 c2; do
+    timeout -k 10 500 python bench.py --workload $w --skip-cpu > $OUT/bench_$w.log 2>&1 || exit 1
+    echo "$w $(tail -1 $OUT/bench_$w.log | cut -c1-120)"
+  done
+  exit 0
+}
+
 case "${1:-}" in
-  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22) "$1" ;;
-  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22}" >&2; exit 2 ;;
+  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23) "$1" ;;
+  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23}" >&2; exit 2 ;;
 esac
