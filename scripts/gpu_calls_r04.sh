@@ -459,7 +459,21 @@ c23() {
   exit 0
 }
 
+c24() {
+  # round 4, final library: configs[2] with one pipeline against two, alternating three times
+  set -u
+  export OUT=gpurun_out/r04x TMPDIR=/tmp
+  mkdir -p $OUT
+  for r in 1 2 3; do
+    for p in 1 2; do
+      timeout -k 10 400 python bench.py --skip-cpu --skip-kernel --pipelines $p > $OUT/c3_p${p}_$r.log 2>&1 || exit 1
+      echo "p$p $(tail -1 $OUT/c3_p${p}_$r.log | cut -c1-110)"
+    done
+  done
+  exit 0
+}
+
 case "${1:-}" in
-  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23) "$1" ;;
-  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23}" >&2; exit 2 ;;
+  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24) "$1" ;;
+  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24}" >&2; exit 2 ;;
 esac
