@@ -473,7 +473,23 @@ c24() {
   exit 0
 }
 
+c25() {
+  # round 4, final library: the trunk conv's prefetch distances again (weight ring 2 / 3 / 4
+  # steps ahead, input slices 1 / 2 chunks ahead) -- B = 1,024 evaluation time, alternating
+  set -u -o pipefail
+  export OUT=gpurun_out/r04y TMPDIR=/tmp
+  mkdir -p $OUT
+  for r in 1 2; do
+    for v in tree pd2 pd4 ipd1; do
+      if [ $v = tree ]; then L=""; else L=expbuild/$v/libaz_othello.so; fi
+      AZ_LIB_PATH=$L timeout -k 10 200 python scripts/net_time.py 1024 40 | sed "s/^{/{\"variant\": \"$v\", /" >> $OUT/net.jsonl || exit 1
+    done
+  done
+  cat $OUT/net.jsonl
+  exit 0
+}
+
 case "${1:-}" in
-  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24) "$1" ;;
-  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24}" >&2; exit 2 ;;
+  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25) "$1" ;;
+  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25}" >&2; exit 2 ;;
 esac
