@@ -409,6 +409,41 @@ def conv_roofline(sp, device, n_boards):
 CALIBRATION_JSON = os.path.join(ROOT, "profiles", "cpu_calibration.json")
 
 
+def trunk_roofline(sp, device, n_boards):
+    """The step's dominant launch since round 4 -- the whole net after the engine's select
+    launch: k_trunk_wino4, the stem, every block conv and the heads in one persistent kernel
+    (FusedInferenceNet.evaluate_into on canonical planes) -- timed with HIP events on its
+    launch stream at the bench's leaf batch.  achieved = the block convs' MFMA FLOP per launch
+    (2*B*64*C*C*9 algorithmic per conv x 16/36 Winograd x 3 fp16x2 products) / the average
+    launch time, against the dense fp16 MFMA peak; the stem and heads (< 1 % of the FLOP) are
+    inside the time but not counted."""
+    net = sp.net
+    if not (hasattr(net, "c1") and getattr(net, "conv_impl", "") == "hip" and net.c1
+            and all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16x2"
+                    for c in list(net.c1) + list(net.c2))):
+        return None
+    C, n_convs = net.c1[0].channels, 2 * len(net.c1)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randint(-1, 2, (n_boards, 64), generator=g).float().to(device)
+    pr = torch.empty(n_boards, 65, device=device)
+    va = torch.empty(n_boards, device=device)
+    with torch.no_grad():
+        for _ in range(200):  # past the power-management transient
+            net.evaluate_into(x, pr, va)
+        torch.cuda.synchronize()
+        ms = launch_ms(lambda: net.evaluate_into(x, pr, va), 50)
+    flop = 2.0 * n_boards * 64 * C * C * 9 * n_convs
+    mult = 3 * 256 / 576
+    achieved = mult * flop / (ms * 1e-3) / 1e12
+    return {"kernel": "k_trunk_wino4 (az_trunk_wino4_heads_gpu: stem + %d block convs, Winograd "
+                      "F(2x2,3x3) fp16x2, two boards per workgroup, + heads)" % n_convs,
+            "bound": "mfma", "achieved": round(achieved, 1), "peak": MFMA16_PEAK,
+            "unit": "TFLOP/s", "frac": round(achieved / MFMA16_PEAK, 4), "traffic": None,
+            "boards": n_boards, "avg_launch_ms": round(ms, 4), "conv_flop_per_launch": flop,
+            "mfma_flop_per_algorithmic_flop": round(mult, 4),
+            "us_per_conv": round(ms * 1e3 / n_convs, 2)}
+
+
 def cpu_baseline(net_kind, sims, seconds, seed=0, start_ply=0, full_games=0):
     """The oracle's restatement of one_self_play (reference algorithm, sequential MCTS,
     batch-1 torch-CPU inference, C board oracle) on one core.  The worker reaches ply
@@ -843,6 +878,10 @@ def main():
     if rank == 0 and not a.skip_kernel and hasattr(sp.net, "c2") \
             and getattr(sp.net, "conv_impl", "") == "hip":
         result["roofline_conv"] = conv_roofline(sp, device, a.games * a.leaves)
+        if a.games * a.leaves <= 4 * torch.cuda.get_device_properties(device).multi_processor_count:
+            rt = trunk_roofline(sp, device, a.games * a.leaves)
+            if rt is not None:
+                result["roofline_trunk"] = rt
     if rank == 0 and not a.skip_cpu:
         result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds,
                                                    a.cpu_workers or host_cpu_share())

@@ -489,7 +489,20 @@ c25() {
   exit 0
 }
 
+c26() {
+  # round 4, final: the default bench line with the new roofline_trunk object (the step's
+  # dominant launch), and the smoke
+  set -u
+  export OUT=gpurun_out/r04z TMPDIR=/tmp
+  mkdir -p $OUT
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
+  tail -1 $OUT/smoke.log
+  timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || exit 1
+  tail -1 $OUT/bench.log | cut -c1-200
+  exit 0
+}
+
 case "${1:-}" in
-  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25) "$1" ;;
-  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25}" >&2; exit 2 ;;
+  c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25|c26) "$1" ;;
+  *) echo "usage: $0 {c1|c2|c3|c4|c7|c8|c9|c10|c11|c12|c13|c14|c15|c16|c17|c18|c19|c20|c21|c22|c23|c24|c25|c26}" >&2; exit 2 ;;
 esac
