@@ -82,6 +82,7 @@ SIGNATURES = {
     "oth_legal_gpu": [_P, _P, _P, _I64, _P],
     "oth_step_gpu": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
     "oth_d4_gpu": [_P, _P, _P, _I64, _P],
+    "oth_step_io_gpu": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
     "az_engine_create": [ctypes.POINTER(AzConfig), ctypes.POINTER(_P)],
     "az_engine_destroy": [_P],
     "az_engine_geometry": [_P, _P, _P, _P],

@@ -155,6 +155,44 @@ __global__ __launch_bounds__(kBlock) void k_step2(const uint64_t* __restrict__ o
   }
 }
 
+// The ceiling of k_step2's access pattern: the same grid, the same 16-byte own/opp/out,
+// 2-byte act and 4-byte status non-temporal accesses per lane (17 B in, 26 B out per
+// position), no board arithmetic -- each output is a one-instruction function of the inputs
+// so no load is dead.  A measurement probe only (bench.py's roofline.pattern_ceiling_*):
+// how close k_step2 gets to what the box moves for its read/write mix.
+__global__ __launch_bounds__(kBlock) void k_step2_io(const uint64_t* __restrict__ own,
+                                                     const uint64_t* __restrict__ opp,
+                                                     const uint8_t* __restrict__ act,
+                                                     uint64_t* __restrict__ own_o,
+                                                     uint64_t* __restrict__ opp_o,
+                                                     uint64_t* __restrict__ legal_o,
+                                                     uint16_t* __restrict__ status_o,
+                                                     uint32_t n) {
+  const uint32_t pairs = (n + 1) / 2, full = n / 2;
+  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t p_pad = (pairs + kBlock - 1) / kBlock * kBlock;
+  const char* own_b = reinterpret_cast<const char*>(own);
+  const char* opp_b = reinterpret_cast<const char*>(opp);
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < p_pad; j += stride) {
+    const PairIn cur = load_pair(own_b, opp_b, act, j, pairs, full);
+    const uint32_t o16 = j * 16u;
+    char* oo = reinterpret_cast<char*>(own_o) + o16;
+    char* po = reinterpret_cast<char*>(opp_o) + o16;
+    char* lo = reinterpret_cast<char*>(legal_o) + o16;
+    if (j < full) {
+      st_out(cur.b, reinterpret_cast<u64x2*>(oo));
+      st_out(cur.a, reinterpret_cast<u64x2*>(po));
+      st_out(cur.a | cur.b, reinterpret_cast<u64x2*>(lo));
+      st_out(cur.c, reinterpret_cast<uint32_t*>(status_o) + j);
+    } else if (j < pairs) {
+      *reinterpret_cast<uint64_t*>(oo) = cur.b.x;
+      *reinterpret_cast<uint64_t*>(po) = cur.a.x;
+      *reinterpret_cast<uint64_t*>(lo) = cur.a.x | cur.b.x;
+      status_o[2u * j] = (uint16_t)cur.c;
+    }
+  }
+}
+
 // One position per lane per iteration (any alignment): lane-contiguous 8-byte
 // (own/opp/legal), 1-byte (act) and 2-byte (status) accesses.
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t* __restrict__ own,
@@ -366,6 +404,26 @@ int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
   else
     hipLaunchKernelGGL(k_step, dim3(grid_for(n)), dim3(kBlock), 0, azc::as_stream(stream),
                        own, opp, act, own_o, opp_o, legal_o, status_o, (uint32_t)n);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+
+int oth_step_io_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                    uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                    int64_t n, void* stream) {
+  AZ_REQUIRE(n >= 0, AZ_ERR_ARG, "oth_step_io_gpu: n < 0");
+  if (n == 0) return AZ_OK;
+  AZ_REQUIRE(own && opp && act && own_o && opp_o && legal_o && status_o, AZ_ERR_ARG,
+             "oth_step_io_gpu: null buffer");
+  AZ_REQUIRE(n < (int64_t(1) << 28), AZ_ERR_ARG, "oth_step_io_gpu: n exceeds 2^28");
+  const auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
+  AZ_REQUIRE(a16(own) && a16(opp) && a16(own_o) && a16(opp_o) && a16(legal_o) &&
+                 (reinterpret_cast<uintptr_t>(act) & 1u) == 0 &&
+                 (reinterpret_cast<uintptr_t>(status_o) & 3u) == 0,
+             AZ_ERR_ARG, "oth_step_io_gpu: needs k_step2's alignment");
+  hipLaunchKernelGGL(k_step2_io, dim3(grid_for((n + 1) / 2, AZ_STEP_GRID_CAP)), dim3(kBlock), 0,
+                     azc::as_stream(stream), own, opp, act, own_o, opp_o, legal_o, status_o,
+                     (uint32_t)n);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -62,8 +62,11 @@ using Scratch = ScratchT<kBoards>;
 // leaves the errors, unpaired chains (this) remove them in every heads test and stress run.
 // An empty asm with the four values as read-write operands stops the pairing; the float
 // operations and their order are unchanged.
+#ifndef AZ_HEADS_UNPAIRED
+#define AZ_HEADS_UNPAIRED 1  // 0: round 3's code (the failing form, for the ISA analysis)
+#endif
 __device__ __forceinline__ void unpaired(float4& a) {
-  asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
+  if constexpr (AZ_HEADS_UNPAIRED) asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
 }
 
 __device__ __forceinline__ float wave_sum(float x) {

@@ -315,6 +315,22 @@ class StepKernelBench:
         assert (self.st[:k].cpu().numpy().view(np.uint16) == cs).all()
         return ms
 
+    def time_io_ms(self, warm=400, reps=100):
+        """The same launches of oth_step_io_gpu: k_step2's grid and access pattern (17 B in,
+        26 B out per position, non-temporal) with no board arithmetic -- the ceiling of the
+        pattern on this box (roofline.pattern_ceiling_*).  Run right after time_ms, so both
+        see the chip in the same state."""
+        nat = self.nat
+        for _ in range(warm):
+            nat.check(nat.lib.oth_step_io_gpu(*self.args), "oth_step_io_gpu")
+        torch.cuda.synchronize()
+        ms = launch_ms(lambda: nat.lib.oth_step_io_gpu(*self.args), reps)
+        # the probe really moved the data (no dead loads): own_o = opp, opp_o = own
+        k = min(self.n, 4096)
+        assert torch.equal(self.outs[0][:k], self.inp[1][:k])
+        assert torch.equal(self.outs[1][:k], self.inp[0][:k])
+        return ms
+
     def release(self):
         self.inp = self.outs = self.st = self.args = None
 
@@ -434,12 +450,23 @@ def trunk_roofline(sp, device, n_boards):
         ms = launch_ms(lambda: net.evaluate_into(x, pr, va), 50)
     flop = 2.0 * n_boards * 64 * C * C * 9 * n_convs
     mult = 3 * 256 / 576
-    achieved = mult * flop / (ms * 1e-3) / 1e12
+    executed = mult * flop / (ms * 1e-3) / 1e12
+    # the whole net's algorithmic FLOP per evaluation (189.0 MFLOP for
+    # AlphaZeroNet(5x128)): stem 3x3 (1 -> C), the block convs, the 1x1 policy (2) + value (1)
+    # convs, pol_fc (128 -> 65), val_fc1 (64 -> 256), val_fc2 (256 -> 1)
+    per_eval = (2 * 64 * C * 9 + 2 * 64 * C * C * 9 * n_convs + 2 * 64 * C * 3
+                + 2 * 128 * 65 + 2 * 64 * 256 + 2 * 256)
+    algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
     return {"kernel": "k_trunk_wino4 (az_trunk_wino4_heads_gpu: stem + %d block convs, Winograd "
                       "F(2x2,3x3) fp16x2, two boards per workgroup, + heads)" % n_convs,
-            "bound": "mfma", "achieved": round(achieved, 1), "peak": MFMA16_PEAK,
-            "unit": "TFLOP/s", "frac": round(achieved / MFMA16_PEAK, 4), "traffic": None,
+            "bound": "mfma", "achieved": round(algorithmic, 1), "peak": MFMA16_PEAK,
+            "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": None,
+            "achieved_basis": "algorithmic: the net's %.1f MFLOP per evaluation x boards / launch "
+                              "time" % (per_eval / 1e6),
+            "mfma_executed_tflops": round(executed, 1),
+            "frac_mfma_executed": round(executed / MFMA16_PEAK, 4),
             "boards": n_boards, "avg_launch_ms": round(ms, 4), "conv_flop_per_launch": flop,
+            "algorithmic_flop_per_eval": per_eval,
             "mfma_flop_per_algorithmic_flop": round(mult, 4),
             "us_per_conv": round(ms * 1e3 / n_convs, 2)}
 
@@ -771,6 +798,7 @@ def main():
     if rank == 0 and not a.skip_kernel:
         kb = StepKernelBench(a.kernel_n, device)
         ms_step_kernel = kb.time_ms()
+        ms_io_kernel = kb.time_io_ms()
     sp.step(warmup_run)
     barrier()
     prof = _ProfilerWindow()  # AZ_PROF_WINDOW=1: rocprofv3 --selected-regions traces the window only
@@ -872,6 +900,13 @@ def main():
                               "avg_launch_ms_default_events": round(ms_step_fenced, 4),
                               "frac_default_events": round(STEP_BYTES * n / (ms_step_fenced * 1e-3)
                                                            / 1e9 / HBM_PEAK_GBS, 4),
+                              "pattern_ceiling_ms": round(ms_io_kernel, 4),
+                              "pattern_ceiling_GBps": round(STEP_BYTES * n / (ms_io_kernel * 1e-3) / 1e9, 1),
+                              "pattern_ceiling_frac": round(ms_io_kernel / ms, 4),
+                              "pattern_ceiling": "oth_step_io_gpu: the same grid and 17 B in / 26 B "
+                                                 "out non-temporal accesses with no board "
+                                                 "arithmetic, timed right after; "
+                                                 "pattern_ceiling_frac = its time / k_step2's",
                               "avg_launch_ms_after_selfplay": round(ms_hot, 4),
                               "frac_after_selfplay": round(STEP_BYTES * n / (ms_hot * 1e-3)
                                                            / 1e9 / HBM_PEAK_GBS, 4)}

@@ -105,6 +105,14 @@ int oth_step_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
                  int64_t n, void* stream);
 int oth_d4_gpu(const uint64_t* x, const uint8_t* sym, uint64_t* out, int64_t n,
                void* stream);
+/* Measurement probe, not a reference routine: oth_step_gpu's launch and access pattern
+ * (17 B read, 26 B written per position, non-temporal, k_step2's grid) with no board
+ * arithmetic -- own_o = opp, opp_o = own, legal_o = own | opp, status_o = the action pair.
+ * bench.py times it beside oth_step_gpu as the pattern's ceiling on the box.  Needs
+ * k_step2's alignment (AZ_ERR_ARG otherwise). */
+int oth_step_io_gpu(const uint64_t* own, const uint64_t* opp, const uint8_t* act,
+                    uint64_t* own_o, uint64_t* opp_o, uint64_t* legal_o, uint16_t* status_o,
+                    int64_t n, void* stream);
 
 /* ---------------- batched MCTS self-play engine (device) -------------------------
  * G game slots, each with its own flat SoA node arena (the reference's `Node` tree,

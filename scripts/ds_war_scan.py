@@ -1,0 +1,199 @@
+"""Scan gfx950 machine code for an LDS store whose data VGPRs are overwritten before the store
+is known complete ("The heads' store-data overwrite").
+
+For every `ds_write*` (and `ds_write2*`), the data VGPRs are the operands after the address.
+The store stays "in flight" until an `s_waitcnt` whose lgkmcnt(N) leaves at most N younger
+LGKM operations outstanding (DS operations complete in issue order; SMEM and message ops
+count too).  The scan reports every instruction in that window that WRITES one of the data
+VGPRs: a `ds_read*` / returning DS atomic destination, a vector-memory load destination, or
+a VALU / MFMA destination.  A kernel boundary or an `s_barrier` preceded by lgkmcnt(0) ends
+every window; branches and labels are scanned in layout order (straight-line windows only,
+which is where the compiler schedules a store and the reuse of its registers together).
+
+    python scripts/ds_war_scan.py <file.s | libaz_othello.so> [...]
+
+Input: compiler assembly (.s) or a shared library, whose gfx950 code objects are extracted
+with llvm-objdump --offloading into a temporary directory and disassembled.  Prints one line
+per finding and exits 1 if there is any."""
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+_REG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
+
+
+def regs(op):
+    """VGPR/AGPR set named by one operand string: {('v', n), ...}."""
+    out = set()
+    for m in _REG.finditer(op):
+        if m.group(1):
+            k, a, b = m.group(1), int(m.group(2)), int(m.group(3))
+            out.update((k, i) for i in range(a, b + 1))
+        elif m.group(4):
+            out.add((m.group(4), int(m.group(5))))
+    return out
+
+
+def split_operands(rest):
+    """Operands of one instruction (modifiers like offset:16 stay attached to the last)."""
+    ops, depth, cur = [], 0, ""
+    for ch in rest:
+        if ch == "[":
+            depth += 1
+        elif ch == "]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            ops.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        ops.append(cur.strip())
+    return ops
+
+
+def parse_lines(text):
+    """(function, mnemonic, operand list, raw line) per instruction, in layout order."""
+    fn = "?"
+    for raw in text.splitlines():
+        line = raw.split("//")[0].split(";")[0].rstrip()
+        if not line.strip():
+            continue
+        s = line.strip()
+        if s.endswith(":") and not s.startswith("."):
+            if not s.startswith(".L") and not s.startswith("LBB"):
+                fn = s[:-1]
+            yield fn, ":label", [], raw
+            continue
+        m = re.match(r"^([0-9a-f]+ )?<(.+)>:$", s)  # objdump function header
+        if m:
+            fn = m.group(2)
+            yield fn, ":label", [], raw
+            continue
+        if s.startswith("."):
+            continue
+        parts = s.split(None, 1)
+        mn = parts[0]
+        if not re.match(r"^[sv]_|^ds_|^buffer_|^global_|^flat_|^scratch_", mn):
+            continue
+        yield fn, mn, split_operands(parts[1]) if len(parts) > 1 else [], raw
+
+
+def lgkm_wait(mn, ops):
+    """N of an s_waitcnt's lgkmcnt(N), or None."""
+    if mn != "s_waitcnt":
+        return None
+    m = re.search(r"lgkmcnt\((\d+)\)", " ".join(ops))
+    return int(m.group(1)) if m else None
+
+
+def is_lgkm(mn):
+    return mn.startswith("ds_") or mn.startswith("s_load") or mn.startswith("s_buffer_load") \
+        or mn in ("s_sendmsg", "s_memtime", "s_memrealtime", "s_dcache_inv")
+
+
+def written_vregs(mn, ops):
+    """Vector registers an instruction writes (its destination), if any."""
+    if not ops:
+        return set()
+    if mn.startswith("ds_write") or mn.startswith("ds_store") or "_store" in mn:
+        return set()
+    if mn.startswith("ds_"):
+        if mn.startswith("ds_read") or mn.startswith("ds_load") or "_rtn" in mn \
+                or mn.startswith("ds_swizzle") or mn.startswith("ds_permute") \
+                or mn.startswith("ds_bpermute"):
+            return regs(ops[0])
+        return set()
+    if mn.startswith(("buffer_load", "global_load", "flat_load", "scratch_load")):
+        if " lds" in " ".join(ops) or mn.endswith("_lds"):
+            return set()
+        return regs(ops[0])
+    if "atomic" in mn:
+        return regs(ops[0]) if "glc" in " ".join(ops) or "sc0" in " ".join(ops) else set()
+    if mn.startswith("v_"):
+        if mn.startswith(("v_cmp", "v_readlane", "v_readfirstlane", "v_cmpx")):
+            return set()
+        return regs(ops[0])
+    return set()
+
+
+def store_data(mn, ops):
+    if not (mn.startswith("ds_write") or mn.startswith("ds_store")):
+        return None
+    if mn.startswith("ds_write_addtid"):
+        return regs(ops[0]) if ops else set()
+    return set().union(*[regs(o.split(" offset")[0]) for o in ops[1:]]) if len(ops) > 1 else set()
+
+
+def scan_text(text, where=""):
+    findings = []
+    pending = []  # [fn, store raw line, data regs, younger lgkm ops]
+    for fn, mn, ops, raw in parse_lines(text):
+        if pending and pending[0][0] != fn:
+            pending = []
+        n = lgkm_wait(mn, ops)
+        if n is not None:
+            pending = [p for p in pending if p[3] < n]
+            continue
+        if mn == ":label":
+            continue
+        w = written_vregs(mn, ops)
+        if w:
+            for p in pending:
+                hit = w & p[2]
+                if hit:
+                    findings.append((where, fn, p[1].strip(), raw.strip(), sorted(hit)))
+        if is_lgkm(mn):
+            for p in pending:
+                p[3] += 1
+        d = store_data(mn, ops)
+        if d:
+            pending.append([fn, raw, d, 0])
+    return findings
+
+
+def disassemble_so(path):
+    """gfx950 code objects of a HIP shared library, disassembled (text per object)."""
+    tmp = tempfile.mkdtemp(prefix="dswar_")
+    try:
+        lib = os.path.join(tmp, "lib.so")
+        shutil.copy(path, lib)
+        subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", lib], cwd=tmp, check=True,
+                       capture_output=True)
+        out = []
+        for f in sorted(os.listdir(tmp)):
+            if "amdgcn" in f and "gfx950" in f:
+                r = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950",
+                                    "--no-show-raw-insn", os.path.join(tmp, f)],
+                                   check=True, capture_output=True, text=True)
+                out.append((f, r.stdout))
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def scan_path(path):
+    if path.endswith(".s"):
+        return scan_text(open(path).read(), os.path.basename(path))
+    found = []
+    for name, text in disassemble_so(path):
+        found += scan_text(text, name)
+    return found
+
+
+def main(argv):
+    bad = []
+    for p in argv:
+        bad += scan_path(p)
+    for where, fn, st, wr, hit in bad:
+        print(f"{where}: {fn}\n    store: {st}\n    write: {wr}   regs {hit}")
+    print(f"{len(bad)} finding(s)")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

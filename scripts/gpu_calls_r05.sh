@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round 5's GPU calls (gpurun), one function per call, in the order they ran; each writes
+# under gpurun_out/r05<letter>/ and the summaries that were kept are copied to profiles/.
+#     /usr/local/graft/bin/gpurun --timeout 1200 -- bash scripts/gpu_calls_r05.sh c1
+set -u
+export TMPDIR=/tmp
+
+run() {  # run <name> <timeout> cmd...   (stops the call after a fault / abort / time limit)
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" >> "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "stopping after $name"; exit $rc; fi
+  return $rc
+}
+
+pyt() {  # pyt <name> <timeout> <targets...>
+  local name=$1 t=$2; shift 2
+  run "$name" "$t" python -u -m pytest "$@" -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread
+}
+
+c1() {
+  # the reference-pinned net fixtures, the real-engine world-2 generation, then the default
+  # bench line (pattern ceiling + both trunk fractions)
+  export OUT=gpurun_out/r05a
+  mkdir -p $OUT
+  pyt pytest_new 600 tests/test_net_golden_gpu.py tests/test_dist_gpu.py || exit $?
+  run bench 600 python bench.py
+  # the heads' wrong words: the packed-FP32 -> LDS-store probe, and the paired build's heads tests
+  run pk_ds_hazard 300 ./expbuild/pk_ds_hazard 4000
+  run heads_paired 300 env AZ_LIB_PATH=expbuild/paired/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread \
+    -k "two_board or trunk_heads or fused_heads_bit_identical_to_separate_heads"
+  exit 0
+}
+
+"$@"
