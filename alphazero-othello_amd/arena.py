@@ -74,6 +74,7 @@ class BatchedArena:
                                            for ev in self.eval)
         self.steps_per_graph = max(1, int(steps_per_graph))
         self._graphs = {}
+        self._graph_state = None  # what the cached graphs were captured under (_run)
         self._bounds = (0, n_slots, n_slots)  # (0, end of the first-player half, n)
         self.iterations = 0  # select -> net -> expand iterations run (per searching engine)
 
@@ -113,6 +114,14 @@ class BatchedArena:
             for _ in range(n):
                 self._iteration(plan)
             return
+        # the captured launches freeze each engine's Params (kernel arguments by value) and the
+        # evaluators' buffers: a graph is reused only under the same engine parameters and
+        # simulation count, otherwise the cache is dropped and recaptured
+        key_state = (tuple(e.param_epoch for e in self.eng), self.args["num_simulations"],
+                     tuple(id(ev) for ev in self.eval))
+        if key_state != self._graph_state:
+            self._graphs = {}
+            self._graph_state = key_state
         while n > 0:
             m = self.steps_per_graph if n >= self.steps_per_graph else 1
             g = self._graphs.get((plan, m))

@@ -66,6 +66,9 @@ class Engine:
         cfg.stream_id = int(stream_id)
         cfg.leaves_per_step = int(leaves_per_step)
         self.cfg = cfg
+        # bumped whenever a host call changes the Params the kernels take by value
+        # (defer_moves, set_stem): HIP graphs captured before it are stale
+        self.param_epoch = 0
         self.K = max(1, int(leaves_per_step))
         self.rollout = rollout
         with torch.cuda.device(self.device):
@@ -118,6 +121,7 @@ class Engine:
     # deferred moves (include/az_othello.h): step n's move phase inside step n+1's select launch
     def defer_moves(self, on=True):
         nat.check(nat.lib.az_engine_defer_moves(self.h, int(bool(on))), "az_engine_defer_moves")
+        self.param_epoch += 1
 
     def select_move(self, par):
         nat.check(nat.lib.az_select_move(self.h, nat.ptr(self.nn_in), nat.ptr(self.leaf), int(par),
@@ -155,6 +159,7 @@ class Engine:
         [G*K, C, 8, 8] receives relu(conv3x3(nn_in row) + bias) of every packed row, absmax
         float32 [G*K] each row's max |y|.  The tensors are kept referenced here.  None turns it
         off."""
+        self.param_epoch += 1  # the kernels take Params by value: captured graphs are stale
         if w9 is None:
             self._stem = None
             nat.check(nat.lib.az_engine_set_stem(self.h, None, None, None, None, 0),

@@ -38,9 +38,83 @@ def get_training_data(trajectory, winning_player, lambd: float = 1.0):
     return out
 
 
+# one_self_play's per-process game batch (AZ_DROPIN_BATCH): games played together on the
+# batched engine at the first call, handed out one per call while the policy and args match
+_BATCH = {"key": None, "games": []}
+
+
+def _dropin_batch_size():
+    import os
+
+    return int(os.environ.get("AZ_DROPIN_BATCH", "32"))
+
+
+def _batch_key(board_size, args, policy_state):
+    """Identity of what a batch was played with: the policy class, config, every state_dict
+    tensor (bytes) and the args."""
+    import hashlib
+
+    cls, cfg, sd = policy_state
+    h = hashlib.sha1(repr((board_size, getattr(cls, "__qualname__", str(cls)),
+                           sorted(cfg.items()), sorted((k, repr(v)) for k, v in args.items())))
+                     .encode())
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def _games_from_rows(rows):
+    """Engine sample rows -> one list of reference tuples per game.  A game's rows are
+    contiguous in the sample ring (finish_game reserves them at once) and each starts at the
+    initial position, the only position with four stones."""
+    own = np.asarray(rows["own"]).view(np.uint64)
+    opp = np.asarray(rows["opp"]).view(np.uint64)
+    occ = own | opp
+    stones = np.zeros(len(own), np.int64)
+    for sh in range(64):
+        stones += ((occ >> np.uint64(sh)) & np.uint64(1)).astype(np.int64)
+    starts = list(np.flatnonzero(stones == 4)) + [len(own)]
+    tuples = _rows_to_tuples(rows)
+    return [tuples[a:b] for a, b in zip(starts[:-1], starts[1:])]
+
+
 @torch.no_grad()
 def one_self_play(args_tuple):
-    """One complete game (self_play_worker.py:38-88); returns [(state, pi, G)]."""
+    """One complete game (self_play_worker.py:38-88); returns [(state, pi, G)].
+
+    train.py's spawn pool (train.py:199-225) calls this once per game in each worker
+    process.  By default (AZ_DROPIN_BATCH = 32) the worker's first call plays that many
+    games at once on the batched GPU engine (BatchedSelfPlay: the same search, K =
+    args['num_threads'] virtual-loss leaves per step, Dirichlet root noise, temperature
+    schedule and TD(lambda) targets; its Philox seed drawn from np.random, which the pool's
+    _worker_init seeds) and hands them out one per call while the policy weights and args
+    are unchanged -- games distributed like the reference's, the engine's rate instead of
+    one search at a time.  AZ_DROPIN_BATCH <= 1: one game per call through the drop-in MCTS
+    (np.random draws in the reference's order)."""
+    n = _dropin_batch_size()
+    if n <= 1:
+        return _one_game(args_tuple)
+    board_size, args, policy_state, _ = args_tuple
+    assert board_size == 8
+    key = _batch_key(board_size, args, policy_state)
+    if _BATCH["key"] != key:
+        _BATCH["key"], _BATCH["games"] = key, []
+    if not _BATCH["games"]:
+        policy_class, policy_config, policy_state_dict = policy_state
+        policy = policy_class(**policy_config)
+        policy.load_state_dict(policy_state_dict)
+        policy.eval()
+        seed = int(np.random.randint(0, 2**31 - 1))
+        rows = _local_rows(policy, args, n, None, seed, 0, False, torch.float32)
+        _BATCH["games"] = _games_from_rows(rows)
+        assert len(_BATCH["games"]) == n, (len(_BATCH["games"]), n)
+    return _BATCH["games"].pop(0)
+
+
+@torch.no_grad()
+def _one_game(args_tuple):
+    """One complete game through the drop-in MCTS (self_play_worker.py:38-88)."""
     board_size, args, policy_state, inference_cache = args_tuple
     env = OthelloGame(board_size)
     policy_class, policy_config, policy_state_dict = policy_state

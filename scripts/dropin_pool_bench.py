@@ -71,7 +71,10 @@ def main():
                       "games_per_s": round(games / dt, 4), "plies": plies,
                       "window_s": round(dt, 2),
                       "net": "AlphaZeroNet(5,128) random init, fused HIP inference copy",
-                      "path": "train.py Pool -> one_self_play -> drop-in MCTS (4 leaves/step)"}))
+                      "path": "train.py Pool -> one_self_play (AZ_DROPIN_BATCH games per worker "
+                              "batch on the batched engine; 1 = one game per call through the "
+                              "drop-in MCTS), 4 leaves/step",
+                      "dropin_batch": int(os.environ.get("AZ_DROPIN_BATCH", "32"))}))
 
 
 if __name__ == "__main__":

@@ -64,20 +64,54 @@ __device__ __forceinline__ void produce_store(unsigned addr, float x, float y) {
                  :: "v"(addr), "v"(x), "v"(y) : CLOB);
 }
 
-template <int V>
-__device__ __forceinline__ float4 expect(float x, float y) {
-  if constexpr (V == 5) return {x * y, y * x, y, x};
-  if constexpr (V == 6) return {__fmaf_rn(x, y, y), __fmaf_rn(y, x, x), y, x};
-  return {x + y, y + x, y, x};
+// V == 7: the heads' sequence (heads_az.h val_fc1 quad, round 3's failing build): a packed mul
+// feeding a packed add, an independent packed add into the quad's other half, one SALU, the
+// store -- quad = (x + x*y, y + y*x, 2y, 2x)
+template <>
+__device__ __forceinline__ void produce_store<7>(unsigned addr, float x, float y) {
+  asm volatile(LOAD
+               "v_pk_mul_f32 v[206:207], v[200:201], v[204:205]\n"
+               "v_pk_add_f32 v[200:201], v[200:201], v[206:207]\n"
+               "v_pk_add_f32 v[202:203], v[202:203], v[204:205]\n"
+               "s_add_i32 s0, 0, 0x10200\n"
+               "ds_write_b128 %0, v[200:203]\n s_waitcnt lgkmcnt(0)\n"
+               :: "v"(addr), "v"(x), "v"(y) : CLOB, "v207", "s0");
 }
 
 template <int V>
-__global__ __launch_bounds__(256) void k_probe(const float* __restrict__ in,
+__device__ __forceinline__ float4 expect(float x, float y) {
+  if constexpr (V == 7)  // no contraction: the asm rounds the product, then the sum
+    return {__fadd_rn(x, __fmul_rn(x, y)), __fadd_rn(y, __fmul_rn(y, x)), __fadd_rn(y, y),
+            __fadd_rn(x, x)};
+  if constexpr (V == 5) return {__fmul_rn(x, y), __fmul_rn(y, x), y, x};
+  if constexpr (V == 6) return {__fmaf_rn(x, y, y), __fmaf_rn(y, x, x), y, x};
+  return {__fadd_rn(x, y), __fadd_rn(y, x), y, x};
+}
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+template <int V>
+__global__ __launch_bounds__(512) void k_probe(const float* __restrict__ in,
                                                unsigned* __restrict__ bad,
                                                unsigned* __restrict__ stale, int iters,
                                                int busy) {
   __shared__ float4 buf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w >= 4) {  // MFMA companions (mfma mode): the same SIMDs kept busy with MFMA chains
+    h8 a, b;
+    for (int i = 0; i < 8; ++i) {
+      a[i] = (_Float16)(in[(lane * 8 + i) & 4095]);
+      b[i] = (_Float16)(in[(lane * 8 + i + 99) & 4095]);
+    }
+    f16v acc = {};
+    for (int it = 0; it < iters; ++it)
+      for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+    float sgn = 0.f;
+    for (int e = 0; e < 16; ++e) sgn += acc[e];
+    if (sgn == 12345.f) atomicAdd(&bad[lane], 1u << 30);  // keep the chain alive
+    return;
+  }
   const unsigned addr = (unsigned)(size_t)(&buf[w][lane]);
   float x = in[(blockIdx.x * 256 + threadIdx.x) & 4095];
   float y = in[(blockIdx.x * 256 + threadIdx.x + 1777) & 4095];
@@ -108,7 +142,9 @@ void run(const char* name, int iters, int busy, int blocks, const float* d_in, u
          unsigned* d_stale) {
   CHECK(hipMemset(d_bad, 0, 64 * 4));
   CHECK(hipMemset(d_stale, 0, 64 * 4));
-  hipLaunchKernelGGL(k_probe<V>, dim3(blocks), dim3(256), 0, 0, d_in, d_bad, d_stale, iters, busy);
+  const int threads = busy < 0 ? 512 : 256;  // busy < 0: MFMA companion waves
+  hipLaunchKernelGGL(k_probe<V>, dim3(blocks), dim3(threads), 0, 0, d_in, d_bad, d_stale, iters,
+                     busy < 0 ? 0 : busy);
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   unsigned bad[64], stale[64];
@@ -131,7 +167,7 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 2000;
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const int blocks = cus * 8;  // 8 four-wave workgroups per CU: 8 waves per SIMD
+  const int blocks = cus * 4;  // up to 4 workgroups per CU (8 waves per SIMD with companions)
   std::vector<float> h(4096);
   for (int i = 0; i < 4096; ++i) h[i] = 0.001f * (float)((i * 7919) % 4001) - 2.0f;
   float* d_in;
@@ -140,8 +176,10 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&d_bad, 64 * 4));
   CHECK(hipMalloc(&d_stale, 64 * 4));
   CHECK(hipMemcpy(d_in, h.data(), 4096 * 4, hipMemcpyHostToDevice));
-  for (int busy : {0, 8}) {
+  for (int busy : {-1, 8, 0}) {
     for (int nb : {cus, 2 * cus, blocks}) {
+      run<7>("heads sequence: pk_mul, pk_add, pk_add, s_add, ds_write_b128", iters, busy, nb, d_in,
+             d_bad, d_stale);
       run<0>("pk_add -> ds_write_b128", iters, busy, nb, d_in, d_bad, d_stale);
       run<1>("pk_add, s_nop 0, ds_write_b128", iters, busy, nb, d_in, d_bad, d_stale);
       run<2>("pk_add, v_mov, ds_write_b128", iters, busy, nb, d_in, d_bad, d_stale);

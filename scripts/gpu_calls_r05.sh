@@ -23,17 +23,35 @@ pyt() {  # pyt <name> <timeout> <targets...>
 }
 
 c1() {
-  # the reference-pinned net fixtures, the real-engine world-2 generation, then the default
-  # bench line (pattern ceiling + both trunk fractions)
+  # the reference-pinned net fixtures, the real-engine world-2 generation, the ADVICE tests,
+  # then the default bench line (pattern ceiling + both trunk fractions); the heads probes;
+  # the unchanged-pool drop-in rate; a graph-mode kernel trace with graph packet capture off
   export OUT=gpurun_out/r05a
   mkdir -p $OUT
-  pyt pytest_new 600 tests/test_net_golden_gpu.py tests/test_dist_gpu.py || exit $?
+  pyt pytest_new 600 tests/test_net_golden_gpu.py tests/test_dist_gpu.py \
+    tests/test_arena_gpu.py tests/test_callers_gpu.py tests/test_engine_gpu.py || exit $?
   run bench 600 python bench.py
-  # the heads' wrong words: the packed-FP32 -> LDS-store probe, and the paired build's heads tests
-  run pk_ds_hazard 300 ./expbuild/pk_ds_hazard 4000
+  run pk_ds_hazard 120 ./expbuild/pk_ds_hazard 4000
   run heads_paired 300 env AZ_LIB_PATH=expbuild/paired/libaz_othello.so python -u -m pytest \
     tests/test_nn_gpu.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread \
     -k "two_board or trunk_heads or fused_heads_bit_identical_to_separate_heads"
+  run dropin_pool 400 python scripts/dropin_pool_bench.py 8 256 400
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_graph 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof -o run -- python3 bench.py --skip-cpu --steps 400 --warmup 2000
+  exit 0
+}
+
+c2() {
+  # the heads hazard with MFMA companions on the same SIMDs; configs[2]'s leaf batch with two
+  # 1,024-slot pipelines (2,048 games) against the one-pipeline default, same box
+  export OUT=gpurun_out/r05b
+  mkdir -p $OUT
+  run pk_ds_hazard 300 ./expbuild/pk_ds_hazard 4000
+  run bench_1p 300 python bench.py --skip-cpu
+  run bench_2x1024 300 python bench.py --skip-cpu --skip-kernel --games 2048 --pipelines 2
+  run bench_1p_b 300 python bench.py --skip-cpu --skip-kernel
+  run bench_2x1024_b 300 python bench.py --skip-cpu --skip-kernel --games 2048 --pipelines 2
   exit 0
 }
 

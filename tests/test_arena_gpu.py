@@ -112,3 +112,28 @@ def test_arena_graph_replay_equals_oracle(threads):
         exp[2 if r == 0 else (0 if (r == 1) == a_first else 1)] += 1
     assert (wa, wb, dr) == tuple(exp)
     assert plies == exp_plies
+
+
+def test_arena_graphs_follow_simulation_count_changes():
+    """the arena's HIP graphs freeze the engines' Params and the evaluators'
+    buffers; a caller that changes num_simulations between play() calls (bench's warm-up
+    plays 8 sims, then the timed 400) must still get exactly the oracle's matches at the new
+    count -- the graph cache is keyed on what it was captured under."""
+    from mock_policy import MockNet
+
+    args = {"c_puct": 2.0, "num_simulations": 8}
+    arena = BatchedArena(MockNet(1).cuda(), MockNet(2).cuda(), args, n_slots=4,
+                         tie_break=tie_break_lowest)
+    for sims in (8, 24, 8):
+        args["num_simulations"] = sims
+        wa, wb, dr, plies = arena.play(4)
+        exp = [0, 0, 0]
+        exp_plies = []
+        for m in range(4):
+            a_first = m % 2 == 0
+            r, pl = oracle_play_match(1 if a_first else 2, 2 if a_first else 1, args)
+            exp_plies.append(pl)
+            exp[2 if r == 0 else (0 if (r == 1) == a_first else 1)] += 1
+        assert (wa, wb, dr) == tuple(exp), sims
+        assert plies == exp_plies, sims
+        assert arena._graph_state[1] == sims

@@ -127,3 +127,47 @@ def test_dropin_net_search_graph_replay_equals_eager(threads, monkeypatch):
             assert np.array_equal(a[0], b[0]), ply
             assert a[1] == b[1] and a[2] == b[2], ply
             assert np.array_equal(a[3], b[3]), ply
+
+
+def _endgame_positions(n, max_empty, seed):
+    """Positions of seeded random playouts with at most max_empty empty squares left and a
+    placement for the side to move (most simulations from them end on terminal nodes)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        own, opp, player = 0x0000000810000000, 0x0000001008000000, 1
+        while True:
+            lg = ob.legal(own, opp)
+            empty = 64 - bin(own | opp).count("1")
+            if lg and empty <= max_empty:
+                out.append((own, opp, player))
+                break
+            if not lg and not ob.legal(opp, own):
+                break
+            moves = [a for a in range(64) if (lg >> a) & 1] or [64]
+            own, opp = ob.make_move(own, opp, int(rng.choice(moves)))
+            player = -player
+    return out
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_dropin_endgame_searches_terminal_heavy(threads):
+    """the drop-in search raises after 1,000 selects without progress.  Under the
+    reference's settings a host-driven select's descent budget covers every simulation, so
+    terminal-heavy end-game trees (1-4 empty squares: nearly every simulation ends on a
+    terminal node, backed up in place) finish without the guard firing, at the reference's
+    worker count of 4 and at 1 -- visit counts equal to the oracle's."""
+    env = OthelloGameNew(8)
+    for max_empty in (1, 2, 4):
+        for own, opp, player in _endgame_positions(3, max_empty, 17 + max_empty):
+            state = ob.to_state(own, opp, player)
+            args = {"c_puct": 2.0, "num_simulations": 64, "num_threads": threads}
+            mcts = MCTS(env, args, MockPolicy())
+            ref = SeqMCTS(args["c_puct"], 64, _oracle_eval, leaves_per_step=threads)
+            np.random.seed(5)
+            mcts.policy_improve_step(state, player, temp=1.0)
+            np.random.seed(5)
+            ref.search(own, opp, player, 1.0)
+            got = np.array([c.visit_count if c else 0 for c in
+                            (mcts.root.children.get(a) for a in range(65))])
+            assert (got == ref.root_counts()).all(), (max_empty, threads)

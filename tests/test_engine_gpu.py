@@ -140,10 +140,13 @@ def test_selfplay_games_match_reference_on_device():
             assert (smp["z"][mine] == d["z"][sel]).all()
 
 
-def test_drop_in_one_self_play_matches_reference():
+def test_drop_in_one_self_play_matches_reference(monkeypatch):
     """self_play_worker.one_self_play -> MCTS drop-in (GPU engine, host-driven) with the
-    recorded np.random draws replayed: identical training tuples."""
+    recorded np.random draws replayed: identical training tuples (the one-game-per-call path,
+    AZ_DROPIN_BATCH=1)."""
     import self_play_worker
+
+    monkeypatch.setenv("AZ_DROPIN_BATCH", "1")
 
     d = load_golden("selfplay_games.npz")
     for g in (0, 3):
@@ -285,3 +288,53 @@ def test_d4_augment_priors_match_reference_unsymmetrise():
         acts = t["action"][fc:fc + nc].astype(np.int64)
         assert (acts == np.nonzero(valid)[0]).all()
         assert (t["prior"][fc:fc + nc].astype(np.float32) == priors[acts]).all(), g
+
+
+def test_drop_in_one_self_play_batched(monkeypatch):
+    """one_self_play's default per-process batch (AZ_DROPIN_BATCH games on the batched engine
+    at the first call, one returned per call): the games are exactly the engine's games for
+    the seed the first call draws from np.random; a batch is reused only for the same
+    weights and args; every game is a complete reference-format trajectory."""
+    import self_play_worker as spw
+    from Models import FastOthelloNet
+
+    monkeypatch.setenv("AZ_DROPIN_BATCH", "4")
+    spw._BATCH.update(key=None, games=[])
+    torch.manual_seed(0)
+    net = FastOthelloNet(8, 65)
+    ps = (FastOthelloNet, net.get_config(), net.state_dict())
+    args = {"c_puct": 2.0, "num_simulations": 6, "dirichlet_alpha": 1.0,
+            "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
+            "lambda": 0.98}
+    np.random.seed(123)
+    got = [spw.one_self_play((8, args, ps, None)) for _ in range(4)]
+    assert not spw._BATCH["games"]
+    np.random.seed(123)
+    seed = int(np.random.randint(0, 2**31 - 1))
+    want = spw._games_from_rows(spw._local_rows(net, args, 4, None, seed, 0, False,
+                                                torch.float32))
+    assert len(want) == 4
+    # the sample ring records games in completion order: compare as sets of games
+
+    def gkey(game):
+        return b"".join(s.tobytes() + pi.tobytes() + np.float64(z).tobytes() for s, pi, z in game)
+
+    got, want = sorted(got, key=gkey), sorted(want, key=gkey)
+    for g, w in zip(got, want):
+        assert len(g) == len(w) >= 10
+        s0 = g[0][0]
+        assert (s0 != 0).sum() == 4 and s0[3, 4] == 1 and s0[3, 3] == -1
+        for (s, pi, z), (ws, wpi, wz) in zip(g, w):
+            assert s.dtype == np.int8 and s.shape == (8, 8) and pi.shape == (65,)
+            assert np.array_equal(s, ws) and np.array_equal(pi, wpi) and z == wz
+            assert abs(float(pi.sum()) - 1.0) < 1e-5 and -1.0 <= z <= 1.0
+    # the next call starts a new batch; other weights or args never reuse it
+    spw.one_self_play((8, args, ps, None))
+    assert len(spw._BATCH["games"]) == 3
+    key = spw._BATCH["key"]
+    torch.manual_seed(1)
+    ps2 = (FastOthelloNet, net.get_config(), FastOthelloNet(8, 65).state_dict())
+    spw.one_self_play((8, args, ps2, None))
+    assert spw._BATCH["key"] != key and len(spw._BATCH["games"]) == 3
+    spw.one_self_play((8, dict(args, num_simulations=7), ps2, None))
+    assert len(spw._BATCH["games"]) == 3
