@@ -1,5 +1,10 @@
-"""Scan gfx950 machine code for an LDS store whose data VGPRs are overwritten before the store
-is known complete ("The heads' store-data overwrite").
+"""Scan gfx950 machine code for two LDS-store patterns (the two-board heads).
+
+Rule 1 (this module's default CLI mode; diagnostic only): an LDS store whose data VGPRs are
+overwritten before the store is known complete.  The compiler does this routinely (over a
+thousand times in the conv kernels, which pass every bit-exact test), so it is NOT a hazard;
+kept to show that.  Rule 2 (--pk; enforced by tests/test_isa_scan_cpu.py): see
+scan_pk_stores.
 
 For every `ds_write*` (and `ds_write2*`), the data VGPRs are the operands after the address.
 The store stays "in flight" until an `s_waitcnt` whose lgkmcnt(N) leaves at most N younger
@@ -109,7 +114,7 @@ def written_vregs(mn, ops):
             return regs(ops[0])
         return set()
     if mn.startswith(("buffer_load", "global_load", "flat_load", "scratch_load")):
-        if " lds" in " ".join(ops) or mn.endswith("_lds"):
+        if " lds" in " ".join(ops) or "_lds" in mn:
             return set()
         return regs(ops[0])
     if "atomic" in mn:
@@ -127,6 +132,35 @@ def store_data(mn, ops):
     if mn.startswith("ds_write_addtid"):
         return regs(ops[0]) if ops else set()
     return set().union(*[regs(o.split(" offset")[0]) for o in ops[1:]]) if len(ops) > 1 else set()
+
+
+# Rule 2 (the one tests/test_isa_scan_cpu.py enforces on the product library): a multi-dword
+# LDS store (ds_write_b64 / b96 / b128, ds_write2_b64, ds_write2st64_b64) whose data VGPRs were
+# written by a packed-FP32 VALU instruction (v_pk_add / v_pk_mul / v_pk_fma _f32) within the
+# PK_WINDOW instructions before it.  Round 3's two-board heads (heads_az.h with the val_fc1
+# partial-sum quad left to the compiler's SLP pairing) stored wrong words in lanes 48-63 with
+# two workgroups per CU; that build has this pattern at every partial-sum store (30 sites,
+# all in the heads kernels) and the product library has none.
+PK_PRODUCER = re.compile(r"^v_pk_(add|mul|fma)_f32")
+PK_STORES = ("ds_write_b64", "ds_write_b96", "ds_write_b128", "ds_write2_b64",
+             "ds_write2st64_b64")
+PK_WINDOW = 3
+
+
+def scan_pk_stores(text, where="", window=PK_WINDOW):
+    """Rule 2 findings: (where, function, distance, producer line, store line)."""
+    found = []
+    hist = []
+    for fn, mn, ops, raw in parse_lines(text):
+        if mn == ":label":
+            continue
+        if mn in PK_STORES:
+            data = store_data(mn, ops) or set()
+            for dist, (pm, pw, praw) in enumerate(reversed(hist[-window:])):
+                if PK_PRODUCER.match(pm) and pw & data:
+                    found.append((where, fn, dist, praw.strip(), raw.strip()))
+        hist.append((mn, written_vregs(mn, ops), raw))
+    return found
 
 
 def scan_text(text, where=""):
@@ -176,21 +210,36 @@ def disassemble_so(path):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def scan_path(path):
+def texts_of(path):
     if path.endswith(".s"):
-        return scan_text(open(path).read(), os.path.basename(path))
+        return [(os.path.basename(path), open(path).read())]
+    return disassemble_so(path)
+
+
+def scan_path(path):
     found = []
-    for name, text in disassemble_so(path):
+    for name, text in texts_of(path):
         found += scan_text(text, name)
     return found
 
 
 def main(argv):
+    """--pk: rule 2 (packed-FP32 result -> multi-dword LDS store); default: rule 1."""
+    pk = "--pk" in argv
     bad = []
-    for p in argv:
-        bad += scan_path(p)
-    for where, fn, st, wr, hit in bad:
-        print(f"{where}: {fn}\n    store: {st}\n    write: {wr}   regs {hit}")
+    for p in [a for a in argv if a != "--pk"]:
+        if pk:
+            for name, text in texts_of(p):
+                bad += scan_pk_stores(text, name)
+        else:
+            bad += scan_path(p)
+    for f in bad:
+        if pk:
+            where, fn, dist, prod, st = f
+            print(f"{where}: {fn}\n    producer ({dist} between): {prod}\n    store: {st}")
+        else:
+            where, fn, st, wr, hit = f
+            print(f"{where}: {fn}\n    store: {st}\n    write: {wr}   regs {hit}")
     print(f"{len(bad)} finding(s)")
     return 1 if bad else 0
 
