@@ -106,6 +106,18 @@
 #ifndef AZ_W4_TAIL
 #define AZ_W4_TAIL 1
 #endif
+// the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
+// the staged residual in one packed add); 0 = one element at a time (A/B builds)
+#ifndef AZ_W4_EPI_PK
+#define AZ_W4_EPI_PK 0
+#endif
+// the persistent trunk's layer hand-off: a layer's epilogue also writes its output's first two
+// 16-channel slices (channels 0-31, held by the column-block-0 wave) into the input slots and
+// its per-board max |y| into LDS, so the next layer starts transforming without the global
+// round trip of those slices and of its input ranges (same values: bit-identical); 0 = off
+#ifndef AZ_W4_HANDOFF
+#define AZ_W4_HANDOFF 0
+#endif
 
 namespace {
 
@@ -198,8 +210,11 @@ struct W4 {
   static constexpr int RS = RES_BYTES / 16 / THREADS / 8;  // 16-byte pieces per thread per chunk
   // staged only where it fits beside the rest (not split3's three planes: its residual is
   // read from global memory in the epilogue)
-  static constexpr bool RES_FITS = RES_OFF + RES_BYTES <= 160 * 1024;
-  static constexpr int LDS_BYTES = RES_FITS ? RES_OFF + RES_BYTES : RES_OFF;
+  static constexpr bool RES_FITS = RES_OFF + RES_BYTES <= 160 * 1024 - 128;
+  // the persistent trunk's layer hand-off (AZ_W4_HANDOFF): each wave's per-board max |y|,
+  // [wave][board] floats after everything else
+  static constexpr int RNG_OFF = RES_FITS ? RES_OFF + RES_BYTES : RES_OFF;
+  static constexpr int LDS_BYTES = RNG_OFF + 128;
   static constexpr int LD_PER_THREAD = BOARDS * 64 * 4 / THREADS;  // 16-byte loads per chunk
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes of one (chunk, point)
   static constexpr int CHUNKS = C / 16;
@@ -790,7 +805,7 @@ struct Epi {
 // output half I (rows 2ty + I): accumulator element e of row tile rt = tile 32rt + (e&3) +
 // 8(e>>2) + 4h, column co; Y[I][j] = output (2ty + I, 2tx + j); + bias (+ the staged
 // residual), ReLU, store, and the boards' max |y|
-template <class G, int I, bool RES, bool RELU, bool HEADS = false>
+template <class G, int I, bool RES, bool RELU, bool HEADS = false, bool KEEP = false>
 __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __restrict__ res,
                                          float* __restrict__ y, int rt0, int h) {
   constexpr int C = G::C;
@@ -801,6 +816,34 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
       const int T = 32 * (rt0 + t) + (e & 3) + 8 * (e >> 2) + 4 * h;
       const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
       if (bd >= S.nb) continue;
+#if AZ_W4_EPI_PK
+      // the output pair (2tx, 2tx + 1) of row 2ty + I shares its scale, bias and column: one
+      // v_pk_fma_f32 for scale + bias (the power-of-two scaling is exact, so the fused form
+      // rounds like the product then the sum), one packed residual add
+      if constexpr (!HEADS && G::SCALED && (!RES || G::RES_FITS)) {
+        const float u = E.unsc[2 * t + (e >> 3)];
+        f32x2 v = __builtin_elementwise_fma(f32x2{S.Y[I][0][t][e], S.Y[I][1][t][e]},
+                                            f32x2{u, u}, f32x2{E.bv, E.bv});
+        if constexpr (RES) {
+          const float* rp = reinterpret_cast<const float*>(
+              S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx) * C + E.co) * 4);
+          v = v + f32x2{rp[0], rp[C]};
+        }
+        if (RELU) {
+          v.x = fmaxf(v.x, 0.0f);
+          v.y = fmaxf(v.y, 0.0f);
+        }
+        float* yp = &y[((size_t)(S.b0 + bd) * 64 + (2 * ty + I) * 8 + 2 * tx) * C + E.co];
+        yp[0] = v.x;
+        yp[C] = v.y;
+        if constexpr (KEEP) {
+          S.Y[I][0][t][e] = v.x;
+          S.Y[I][1][t][e] = v.y;
+        }
+        E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fmaxf(fabsf(v.x), fabsf(v.y)));
+        continue;
+      }
+#endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int pos = (2 * ty + I) * 8 + 2 * tx + j;
@@ -818,6 +861,7 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
             __builtin_nontemporal_store(v, &y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co]);
           else
             y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
+          if constexpr (KEEP) S.Y[I][j][t][e] = v;
           E.bmax[2 * t + (e >> 3)] = fmaxf(E.bmax[2 * t + (e >> 3)], fabsf(v));
         }
       }
@@ -884,13 +928,22 @@ __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int
 
 // One conv of this workgroup's boards (the whole kernel of k_conv3x3_wino4; the persistent
 // trunk k_trunk_wino4 runs it once per layer on the same boards).
-template <class G, bool RES, bool RELU, bool HEADS = false, bool LAUNDER = false>
+// HIN / HOUT (AZ_W4_HANDOFF, the persistent trunk's layers): HIN = the input's first two
+// slices are already in the input slots and its per-board ranges in LDS (written by the
+// previous layer's HOUT epilogue, ordered by the layer fence); HOUT = write them for the next
+// layer.  Two-board, one-row-tile form only (the trunk's).
+template <class G, bool RES, bool RELU, bool HEADS = false, bool LAUNDER = false,
+          bool HIN = false, bool HOUT = false>
 __device__ __forceinline__ void conv_body(
     const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
     float* __restrict__ in_absmax, float* __restrict__ out_absmax, HeadsOut ho,
     int layer = 0) {
   constexpr int C = G::C;
+  static_assert(!(HIN || HOUT) || (G::BOARDS == 2 && G::NRT == 1 && G::IPD == 1 && G::SCALED &&
+                                   !G::SPLIT && LAUNDER),
+                "the layer hand-off is the persistent two-board fp16x2 trunk's");
+
   extern __shared__ float4 lds4[];
   W4_STAMP(0);
   W4T_STAMP(layer, 0);
@@ -916,6 +969,19 @@ __device__ __forceinline__ void conv_body(
   const int col0 = 32 * cb;
   const int b0 = blockIdx.x * G::BOARDS;
   const int nb = n_boards - b0 < G::BOARDS ? n_boards - b0 : G::BOARDS;
+  // the input range of board bd (< nb): from the previous layer's LDS hand-off (the max of
+  // its waves' maxima: the value the buffer's atomics hold), else the buffer
+  auto in_range = [&](int bd) -> float {
+    if constexpr (HIN) {
+      const float* rng = reinterpret_cast<const float*>(S.lds + G::RNG_OFF);
+      float m = rng[bd];
+#pragma unroll
+      for (int w = 1; w < G::WAVES; ++w) m = fmaxf(m, rng[w * 4 + bd]);
+      return m;
+    } else {
+      return in_absmax[b0 + bd];
+    }
+  };
   S.tid = tid;
   S.b0 = b0;
   S.nb = nb;
@@ -946,7 +1012,7 @@ __device__ __forceinline__ void conv_body(
     if constexpr (G::SCALED) {
       // |V| <= 4 max |x| < 2^(e+2): scaled by 2^(13-e), the transformed inputs stay below
       // 2^15 (fp16's largest power of two)
-      const int e = frexp_exp(bd < nb ? in_absmax[b0 + bd] : 0.0f);
+      const int e = frexp_exp(bd < nb ? in_range(bd) : 0.0f);
       S.vsc[u] = ldexpf(1.0f, 13 - e);
     }
   }
@@ -970,7 +1036,16 @@ __device__ __forceinline__ void conv_body(
   // (the persistent trunk's later layers: the borders are still zero -- interior stores never
   // touch them -- and the layer fence ordered the previous layer's reads)
   const bool fill = !LAUNDER || layer == 0;
-  {
+  if constexpr (HIN) {
+    // chunks 0 and 1 are in the slots already (the previous layer's hand-off, ordered by the
+    // layer fence); chunk 2's slice (stored at the end of chunk 0) and the first weight steps
+    char* in0 = S.lds + G::IN_OFF;
+    load_in<G>(S.ld[0], S.rx, S.goff, lmap<G>(S, 2));
+#pragma unroll
+    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], S.rw, S.wlane, qmap<G>(S, i));
+#pragma unroll
+    for (int u = 0; u < G::TPT; ++u) make_rows<G>(S.rk[u], in0, S.rbase[u], S.cols[u], lmap<G>(S, 0));
+  } else {
     char* in0 = S.lds + G::IN_OFF;
     if (fill)
       for (int i = tid * 16; i < 2 * G::IN_SLOT; i += G::THREADS * 16)
@@ -1031,7 +1106,7 @@ __device__ __forceinline__ void conv_body(
 #pragma unroll
     for (int i = 0; i < 2 * G::NRT; ++i) {
       const int bd = 2 * rt0 + i;
-      const int e = frexp_exp(bd < nb ? in_absmax[b0 + bd] : 0.0f);
+      const int e = frexp_exp(bd < nb ? in_range(bd) : 0.0f);
       E.unsc[i] = ldexpf(1.0f, -(su + 13 - e));
     }
   }
@@ -1069,19 +1144,47 @@ __device__ __forceinline__ void conv_body(
   W4_STAMP(4);
   W4T_STAMP(layer, 2);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
-  epilogue<G, 0, RES, RELU, HEADS>(S, E, res, y, rt0, h);
+  epilogue<G, 0, RES, RELU, HEADS, HOUT>(S, E, res, y, rt0, h);
   if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
   run_group<G, 3, STAGED ? 1 : -1>(S);
   W4_STAMP(5);
   if (STAGED) vm_barrier();
-  epilogue<G, 1, RES, RELU, HEADS>(S, E, res, y, rt0, h);
+  epilogue<G, 1, RES, RELU, HEADS, HOUT>(S, E, res, y, rt0, h);
+  if constexpr (HOUT) {
+    // the next layer's input: its first two slices (channels 0-31 = column block 0's
+    // registers) into the input slots -- free since the last chunk's windows were read,
+    // before this layer's last two barriers -- and each wave's per-board max |y|
+    if (cb == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int T = (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int bd = T >> 4, ty = (T >> 2) & 3, tx = T & 3;
+          if (bd >= nb) continue;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            *reinterpret_cast<float*>(S.lds + G::IN_OFF + (r >> 4) * G::IN_SLOT + bd * G::IN_BOARD +
+                                      (2 * ty + i + 1) * G::IN_ROW +
+                                      col_slot(2 * tx + j + 1) * 64 + (r & 15) * 4) =
+                S.Y[i][j][0][e];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float m = E.bmax[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+      if (lane == 0) reinterpret_cast<float*>(S.lds + G::RNG_OFF)[wave * 4 + i] = m;
+    }
+  }
   if constexpr (HEADS) {
     // in_absmax is consumed (every thread read its entries in the prologue)
     if (threadIdx.x < G::BOARDS && (int)threadIdx.x < nb) in_absmax[b0 + threadIdx.x] = 0.0f;
     heads_epilogue<G>(S, ho, rt0, h, E.co);
     return;
   }
-  if (out_absmax) {  // the next layer's in_absmax: one atomic per (wave, board)
+  if (out_absmax && !HOUT) {  // the next layer's in_absmax: one atomic per (wave, board)
 #pragma unroll
     for (int i = 0; i < 2 * G::NRT; ++i) {
       float m = E.bmax[i];
@@ -1266,20 +1369,41 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   const float* h = a.h_in;
   int ob = 0;
   const int n_loop = EPI ? a.n_convs - 1 : a.n_convs;
+  constexpr bool HO = AZ_W4_HANDOFF != 0;
   for (int i = 0; i < n_loop; ++i) {
     if (i > 0) layer_fence();
+    // a conv whose output the next conv reads hands it off through LDS (every conv but the
+    // launch's last); the first conv reads the stem's output from memory
+    const bool hout = HO && (i + 1 < a.n_convs);
     if ((i & 1) == 0) {
-      conv_body<G, false, true, false, true>(h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]),
-                                             nullptr, a.t, a.n_boards,
-                                             a.amax[0], a.amax[1], HeadsOut{}, i);
+      if (i == 0 && hout)
+        conv_body<G, false, true, false, true, false, HO>(
+            h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards, a.amax[0],
+            a.amax[1], HeadsOut{}, i);
+      else if (i == 0)
+        conv_body<G, false, true, false, true>(h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]),
+                                               nullptr, a.t, a.n_boards,
+                                               a.amax[0], a.amax[1], HeadsOut{}, i);
+      else if (hout)
+        conv_body<G, false, true, false, true, HO, HO>(
+            h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards, a.amax[0],
+            a.amax[1], HeadsOut{}, i);
+      else
+        conv_body<G, false, true, false, true, HO, false>(
+            h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards, a.amax[0],
+            a.amax[1], HeadsOut{}, i);
     } else {
       // the last layer of a HEADS launch keeps no range (nothing reads its output as a
       // conv input): amax[0] stays as the stem / caller left it
       const bool last_heads = HEADS && i == a.n_convs - 1;
-      conv_body<G, true, true, false, true>(a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h,
-                                            a.hb[ob], a.n_boards,
-                                            a.amax[1], last_heads ? nullptr : a.amax[0],
-                                            HeadsOut{}, i);
+      if (hout)
+        conv_body<G, true, true, false, true, HO, HO>(
+            a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h, a.hb[ob], a.n_boards, a.amax[1],
+            last_heads ? nullptr : a.amax[0], HeadsOut{}, i);
+      else
+        conv_body<G, true, true, false, true, HO, false>(
+            a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h, a.hb[ob], a.n_boards, a.amax[1],
+            last_heads ? nullptr : a.amax[0], HeadsOut{}, i);
       h = a.hb[ob];
       ob ^= 1;
     }
@@ -1287,8 +1411,9 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   if constexpr (EPI) {
     layer_fence();  // the last block's first conv output (t) visible to this workgroup
     const int i = a.n_convs - 1;
-    conv_body<G, true, true, true, true>(a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h,
-                                         nullptr, a.n_boards, a.amax[1], nullptr, ho, i);
+    conv_body<G, true, true, true, true, HO, false>(a.t, uniform_ptr(a.wq[i]),
+                                                    uniform_ptr(a.bias[i]), h, nullptr,
+                                                    a.n_boards, a.amax[1], nullptr, ho, i);
   } else if constexpr (HEADS) {
     layer_fence();  // the last layer's stores drained and visible to this workgroup's reads
     trunk_heads<G>(h, a.n_boards, ho);

@@ -55,4 +55,32 @@ c2() {
   exit 0
 }
 
+c3() {
+  # the layer hand-off (AZ_W4_HANDOFF=1) bit for bit against the layer launches and the
+  # reference fixtures; then the product, the packed epilogue (AZ_W4_EPI_PK=1) and the
+  # hand-off timed alternately on one box
+  export OUT=gpurun_out/r05c
+  mkdir -p $OUT
+  run hoff_tests 400 env AZ_LIB_PATH=expbuild/hoff/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread -k "persistent or trunk_heads or golden or matches" \
+    || exit $?
+  for i in 1 2; do
+    run net_base 120 python scripts/net_time.py 1024 40
+    run net_epk 120 env AZ_LIB_PATH=expbuild/epk/libaz_othello.so python scripts/net_time.py 1024 40
+    run net_hoff 120 env AZ_LIB_PATH=expbuild/hoff/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  exit 0
+}
+
+c4() {
+  # the one-game-per-call drop-in (AZ_DROPIN_BATCH=1) re-measured with this library: one game
+  # through the unchanged caller, and train.py's pool of 8 workers
+  export OUT=gpurun_out/r05d
+  mkdir -p $OUT
+  run dropin 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_bench.py
+  run dropin_pool_1 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_pool_bench.py 8 16 400
+  exit 0
+}
+
 "$@"
