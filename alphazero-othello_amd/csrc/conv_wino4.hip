@@ -99,6 +99,12 @@
 #ifndef AZ_W4_MIX
 #define AZ_W4_MIX AZ_W4_PK
 #endif
+// the remaining two-wide adds, products and FMAs of the input transform and the fold as one
+// packed instruction each (inline asm; the compiler emits about a third of them as two
+// scalar ops, profiles/r05_isa_mix.txt); 0 = the plain vector expressions (A/B builds)
+#ifndef AZ_W4_PK2
+#define AZ_W4_PK2 0
+#endif
 // the layer's last two chunks skip the pipeline's look-ahead past the end (clamped duplicates:
 // input slices, their LDS stores and window reads, the last chunk's weight steps, transform
 // and A fragments) -- none of it was ever used: -1.25 % per evaluation at B = 1,024, outputs
@@ -107,16 +113,18 @@
 #define AZ_W4_TAIL 1
 #endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
-// the staged residual in one packed add); 0 = one element at a time (A/B builds)
+// the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
+// + heads launch, same box (profiles/r05_conv_micro_ab.json); 0 = one element at a time
 #ifndef AZ_W4_EPI_PK
-#define AZ_W4_EPI_PK 0
+#define AZ_W4_EPI_PK 1
 #endif
 // the persistent trunk's layer hand-off: a layer's epilogue also writes its output's first two
 // 16-channel slices (channels 0-31, held by the column-block-0 wave) into the input slots and
 // its per-board max |y| into LDS, so the next layer starts transforming without the global
-// round trip of those slices and of its input ranges (same values: bit-identical); 0 = off
+// round trip of those slices and of its input ranges (same values: bit-identical): 411.0-411.5
+// -> 408.0-410.1 us per launch (profiles/r05_conv_micro_ab.json); 0 = off
 #ifndef AZ_W4_HANDOFF
-#define AZ_W4_HANDOFF 0
+#define AZ_W4_HANDOFF 1
 #endif
 
 namespace {
@@ -425,11 +433,41 @@ __device__ __forceinline__ void read_rows_k(f32x2 (&d)[8], const char* lds, cons
   }
 }
 
+// a + b, a * b and fma(a, b, c) on f32x2 as one packed instruction (AZ_W4_PK2), else the
+// vector expressions; the same IEEE results element by element
+__device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
+#if AZ_W4_PK2
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return a + b;
+#endif
+}
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
+#if AZ_W4_PK2
+  f32x2 r;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return a * b;
+#endif
+}
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+#if AZ_W4_PK2
+  f32x2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return __builtin_elementwise_fma(a, b, c);
+#endif
+}
+
 template <int KK>
 __device__ __forceinline__ void combine_k(f32x2 (&rk)[4], const f32x2 (&d)[8], float vsc) {
   const f32x2 fa = {grp_sa(KK) * vsc, grp_sa(KK) * vsc}, fb = {grp_sb(KK) * vsc, grp_sb(KK) * vsc};
 #pragma unroll
-  for (int b = 0; b < 4; ++b) rk[b] = __builtin_elementwise_fma(fb, d[4 + b], fa * d[b]);
+  for (int b = 0; b < 4; ++b) rk[b] = pk_fma(fb, d[4 + b], pk_mul(fa, d[b]));
 }
 
 // a - b on an f32x2 as ONE v_pk_add_f32 with b negated: the compiler splits a two-wide
@@ -449,7 +487,7 @@ __device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
 template <int l>
 __device__ __forceinline__ f32x2 col_comb(const f32x2 (&rk)[4]) {
   if constexpr (l == 0) return pk_sub(rk[0], rk[2]);
-  if constexpr (l == 1) return rk[1] + rk[2];
+  if constexpr (l == 1) return pk_add(rk[1], rk[2]);
   if constexpr (l == 2) return pk_sub(rk[2], rk[1]);
   return pk_sub(rk[1], rk[3]);
 }
@@ -458,7 +496,7 @@ __device__ __forceinline__ f32x2 col_comb(const f32x2 (&rk)[4]) {
 template <class G>
 __device__ __forceinline__ void put(char* slab, f32x2 v, float vsc) {
   if constexpr (G::MODE == AZ_CONV_FP16X2) {
-    const f32x2 vs = v * vsc;  // exact: a power of two
+    const f32x2 vs = v * vsc;  // exact: a power of two (1 in the DIET path: folded away)
     const f16x2 hi = __builtin_convertvector(vs, f16x2);
 #if AZ_W4_MIX
     // lo = RN16(vs - hi) per element by the mixed-precision FMA (hi read as f16, vs - hi
@@ -512,26 +550,26 @@ __device__ __forceinline__ void fold(f32x16 (&acc)[4][G::NRT], f32x16 (&Y)[2][2]
     for (int e = 0; e < 16; e += 2) {
       const f32x2 m0 = get(acc[0][t], e), m1 = get(acc[1][t], e), m2 = get(acc[2][t], e),
                   m3 = get(acc[3][t], e);
-      const f32x2 t0 = (m0 + m1) + m2, t1 = sub(sub(m1, m2), m3);
+      const f32x2 t0 = pk_add(pk_add(m0, m1), m2), t1 = sub(sub(m1, m2), m3);
       if constexpr (K == 0 && G::NG == 4) {
         set(Y[0][0][t], e, t0);
         set(Y[0][1][t], e, t1);
       } else if constexpr (K == 0) {  // NG = 1: Y starts at zero (rows of other workgroups)
-        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
-        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
+        set(Y[0][0][t], e, pk_add(get(Y[0][0][t], e), t0));
+        set(Y[0][1][t], e, pk_add(get(Y[0][1][t], e), t1));
       } else if constexpr (K == 1) {
-        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
-        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
+        set(Y[0][0][t], e, pk_add(get(Y[0][0][t], e), t0));
+        set(Y[0][1][t], e, pk_add(get(Y[0][1][t], e), t1));
         if constexpr (G::NG == 4) {
           set(Y[1][0][t], e, t0);
           set(Y[1][1][t], e, t1);
         } else {
-          set(Y[1][0][t], e, get(Y[1][0][t], e) + t0);
-          set(Y[1][1][t], e, get(Y[1][1][t], e) + t1);
+          set(Y[1][0][t], e, pk_add(get(Y[1][0][t], e), t0));
+          set(Y[1][1][t], e, pk_add(get(Y[1][1][t], e), t1));
         }
       } else if constexpr (K == 2) {
-        set(Y[0][0][t], e, get(Y[0][0][t], e) + t0);
-        set(Y[0][1][t], e, get(Y[0][1][t], e) + t1);
+        set(Y[0][0][t], e, pk_add(get(Y[0][0][t], e), t0));
+        set(Y[0][1][t], e, pk_add(get(Y[0][1][t], e), t1));
         set(Y[1][0][t], e, sub(get(Y[1][0][t], e), t0));
         set(Y[1][1][t], e, sub(get(Y[1][1][t], e), t1));
       } else {

@@ -8,7 +8,23 @@ export TMPDIR=/tmp
 run() {  # run <name> <timeout> cmd...   (stops the call after a fault / abort / time limit)
   local name=$1 t=$2; shift 2
   echo "=== $name: $*" | tee -a $OUT/steps.log
-  timeout -k 10 "$t" "$@" >> "$OUT/$name.log" 2>&1
+  timeout -k 10 "$t" c5() {
+  # the whole GPU suite and smoke() on the library with the epilogue pairs and the layer
+  # hand-off on; the bench line; the unchanged-caller drop-in re-measured (c4's steps)
+  export OUT=gpurun_out/r05e
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench 600 python bench.py
+  run net_base0 120 env AZ_LIB_PATH=expbuild/base0/libaz_othello.so python scripts/net_time.py 1024 40
+  run net_tree 120 python scripts/net_time.py 1024 40
+  run dropin 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_bench.py
+  run dropin_pool_1 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_pool_bench.py 8 16 400
+  exit 0
+}
+
+"$@" >> "$OUT/$name.log" 2>&1
   local rc=$?
   echo "=== $name rc=$rc" | tee -a $OUT/steps.log
   tail -3 "$OUT/$name.log"
@@ -58,7 +74,7 @@ c2() {
 c3() {
   # the layer hand-off (AZ_W4_HANDOFF=1) bit for bit against the layer launches and the
   # reference fixtures; then the product, the packed epilogue (AZ_W4_EPI_PK=1) and the
-  # hand-off timed alternately on one box
+  # hand-off and the packed transform ops (AZ_W4_PK2=1) timed alternately on one box
   export OUT=gpurun_out/r05c
   mkdir -p $OUT
   run hoff_tests 400 env AZ_LIB_PATH=expbuild/hoff/libaz_othello.so python -u -m pytest \
@@ -69,6 +85,7 @@ c3() {
     run net_base 120 python scripts/net_time.py 1024 40
     run net_epk 120 env AZ_LIB_PATH=expbuild/epk/libaz_othello.so python scripts/net_time.py 1024 40
     run net_hoff 120 env AZ_LIB_PATH=expbuild/hoff/libaz_othello.so python scripts/net_time.py 1024 40
+    run net_pk2 120 env AZ_LIB_PATH=expbuild/pk2/libaz_othello.so python scripts/net_time.py 1024 40
   done
   exit 0
 }
