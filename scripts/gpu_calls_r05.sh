@@ -8,23 +8,7 @@ export TMPDIR=/tmp
 run() {  # run <name> <timeout> cmd...   (stops the call after a fault / abort / time limit)
   local name=$1 t=$2; shift 2
   echo "=== $name: $*" | tee -a $OUT/steps.log
-  timeout -k 10 "$t" c5() {
-  # the whole GPU suite and smoke() on the library with the epilogue pairs and the layer
-  # hand-off on; the bench line; the unchanged-caller drop-in re-measured (c4's steps)
-  export OUT=gpurun_out/r05e
-  mkdir -p $OUT
-  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
-    --timeout-method thread || exit $?
-  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-  run bench 600 python bench.py
-  run net_base0 120 env AZ_LIB_PATH=expbuild/base0/libaz_othello.so python scripts/net_time.py 1024 40
-  run net_tree 120 python scripts/net_time.py 1024 40
-  run dropin 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_bench.py
-  run dropin_pool_1 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_pool_bench.py 8 16 400
-  exit 0
-}
-
-"$@" >> "$OUT/$name.log" 2>&1
+  timeout -k 10 "$t" "$@" >> "$OUT/$name.log" 2>&1
   local rc=$?
   echo "=== $name rc=$rc" | tee -a $OUT/steps.log
   tail -3 "$OUT/$name.log"
@@ -95,6 +79,22 @@ c4() {
   # through the unchanged caller, and train.py's pool of 8 workers
   export OUT=gpurun_out/r05d
   mkdir -p $OUT
+  run dropin 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_bench.py
+  run dropin_pool_1 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_pool_bench.py 8 16 400
+  exit 0
+}
+
+c5() {
+  # the whole GPU suite and smoke() on the library with the epilogue pairs and the layer
+  # hand-off on; the bench line; the unchanged-caller drop-in re-measured (c4's steps)
+  export OUT=gpurun_out/r05e
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench 600 python bench.py
+  run net_base0 120 env AZ_LIB_PATH=expbuild/base0/libaz_othello.so python scripts/net_time.py 1024 40
+  run net_tree 120 python scripts/net_time.py 1024 40
   run dropin 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_bench.py
   run dropin_pool_1 400 env AZ_DROPIN_BATCH=1 python scripts/dropin_pool_bench.py 8 16 400
   exit 0
