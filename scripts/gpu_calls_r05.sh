@@ -100,4 +100,31 @@ c5() {
   exit 0
 }
 
+c6() {
+  # the final library: the heads check build's stress (every differing value-path word
+  # printed), the persistent trunk's SQ / TA counters (one group per --pmc pass), and a
+  # graph-mode kernel trace of the bench (graph packet capture off, r05_tracer_fault_decode)
+  export OUT=gpurun_out/r05f
+  mkdir -p $OUT
+  K="persistent_trunk or trunk_heads or fused_heads or two_board"
+  run hchk 400 env AZ_LIB_PATH=expbuild/hchk/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py -m gpu -v -s -p no:cacheprovider --timeout 120 --timeout-method thread \
+    -k "$K"
+  echo "HEADS_CHECK lines: $(grep -c HEADS_CHECK $OUT/hchk.log)" | tee -a $OUT/steps.log
+  i=0
+  for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC" \
+             "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU" \
+             "GRBM_GUI_ACTIVE GRBM_COUNT TA_BUSY_avr TA_TA_BUSY_sum" \
+             "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_VMEM SQ_VALU_MFMA_COEXEC_CYCLES" \
+             "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    run sq_trunk_$i 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq_trunk_$i -o pmc -- \
+      python3 scripts/trunk_one.py 1024 20 calib || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_graph 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof -o run -- python3 bench.py --skip-cpu --steps 400 --warmup 2000
+  exit 0
+}
+
 "$@"
