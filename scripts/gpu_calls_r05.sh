@@ -127,4 +127,26 @@ c6() {
   exit 0
 }
 
+c7() {
+  # the N > 1 bench path rehearsed on the one-GPU box (AZ_BENCH_REHEARSE=1: every rank on
+  # cuda:0, gloo collectives): torchrun world 2 and world 4, the driver's command shape
+  export OUT=gpurun_out/r05g
+  mkdir -p $OUT
+  run rehearse_w2 400 env AZ_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --skip-cpu
+  run rehearse_w4 500 env AZ_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --skip-cpu \
+    --steps 2000
+  # where the persistent trunk's vector-memory requests are served: L1 accesses and misses
+  # (requests to L2), L2 hits and misses
+  i=0
+  for grp in "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum" \
+             "TCP_TCC_WRITE_REQ_sum TCC_REQ_sum TCC_EA0_RDREQ_sum"; do
+    i=$((i+1))
+    run l1l2_trunk_$i 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/l1l2_trunk_$i -o pmc -- \
+      python3 scripts/trunk_one.py 1024 20 || exit $?
+  done
+  exit 0
+}
+
 "$@"
