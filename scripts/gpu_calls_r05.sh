@@ -149,4 +149,20 @@ c7() {
   exit 0
 }
 
+c8() {
+  # the next layer's first weight steps requested before the layer fence (AZ_W4_WPRE=1):
+  # bit-identity tests, then timed against the product alternately
+  export OUT=gpurun_out/r05h
+  mkdir -p $OUT
+  run wpre_tests 400 env AZ_LIB_PATH=expbuild/wpre/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread -k "persistent or trunk_heads or golden or matches" \
+    || exit $?
+  for i in 1 2 3; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    run net_wpre 120 env AZ_LIB_PATH=expbuild/wpre/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  exit 0
+}
+
 "$@"
