@@ -101,7 +101,8 @@
 #endif
 // the remaining two-wide adds, products and FMAs of the input transform and the fold as one
 // packed instruction each (inline asm; the compiler emits about a third of them as two
-// scalar ops, profiles/r05_isa_mix.txt); 0 = the plain vector expressions (A/B builds)
+// scalar ops, profiles/r05_isa_mix.txt): 9 % less loop VALU but twice the hazard s_nops,
+// +0.3 % per launch (profiles/r05_conv_micro_ab.json); 0 = the plain vector expressions
 #ifndef AZ_W4_PK2
 #define AZ_W4_PK2 0
 #endif
