@@ -165,4 +165,15 @@ c8() {
   exit 0
 }
 
+c9() {
+  # the round's final tree: the whole GPU suite, smoke() and the default bench line
+  export OUT=gpurun_out/r05i
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench 600 python bench.py
+  exit 0
+}
+
 "$@"
