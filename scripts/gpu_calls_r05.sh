@@ -176,4 +176,16 @@ c9() {
   exit 0
 }
 
+c10() {
+  # the other workloads on the final library (README quoted round 4's): configs[1] (c2),
+  # configs[3] (c4), configs[4] (c5), the arena
+  export OUT=gpurun_out/r05j
+  mkdir -p $OUT
+  run c2 500 python bench.py --workload c2 --skip-cpu --skip-kernel
+  run c4 500 python bench.py --workload c4 --skip-cpu --skip-kernel
+  run c5 500 python bench.py --workload c5 --skip-cpu --skip-kernel
+  run arena 600 python bench.py --workload arena --matches 1024
+  exit 0
+}
+
 "$@"
