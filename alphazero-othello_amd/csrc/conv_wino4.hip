@@ -67,7 +67,9 @@
 // experiment hooks (scripts/build_variants.py builds with bits set; results wrong):
 // 1 = no weight loads in the loop, 2 = no transform / input work in the loop, 4 = no MFMAs,
 // 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads, 32 = weight loads by the
-// first row tile's waves only (the other half reuses stale fragments).  Product: 0.
+// first row tile's waves only (the other half reuses stale fragments), 64 = no input-slice
+// loads / LDS stores in the loop (the windows read stale slots), 128 = no global stores of a
+// non-residual conv's output.  Product: 0.
 #ifndef AZ_W4_EXP
 #define AZ_W4_EXP 0
 #endif
@@ -112,6 +114,11 @@
 // bit-identical (profiles/r04_conv_tail_ab.json); 0 = the uniform look-ahead (A/B builds)
 #ifndef AZ_W4_TAIL
 #define AZ_W4_TAIL 1
+#endif
+// the persistent trunk's layer input resident in LDS (see conv_body): 0 = the per-chunk input
+// slices (A/B builds)
+#ifndef AZ_W4_RESIDENT
+#define AZ_W4_RESIDENT 0
 #endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
 // the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
@@ -224,6 +231,14 @@ struct W4 {
   // [wave][board] floats after everything else
   static constexpr int RNG_OFF = RES_FITS ? RES_OFF + RES_BYTES : RES_OFF;
   static constexpr int LDS_BYTES = RNG_OFF + 128;
+  // the resident layout (AZ_W4_RESIDENT, the persistent trunk): V buffer 0, the layer's whole
+  // input X = [board][64 positions][C] fp32 (channel chunk slots swizzled by column pair,
+  // xoff), V buffer 1 -- so a board-edge window's out-of-board rows and columns land in
+  // finite words (X, or V's fp16 pairs, never an fp32 Inf / NaN pattern) and are masked
+  static constexpr int XOFF = BUF, XBYTES = BOARDS * 64 * C * 4, V1R = BUF + XBYTES;
+  static constexpr int RSD_BYTES = 2 * BUF + XBYTES;
+  static constexpr int TRUNK_LDS =
+      AZ_W4_RESIDENT && RSD_BYTES > LDS_BYTES ? RSD_BYTES : LDS_BYTES;
   static constexpr int LD_PER_THREAD = BOARDS * 64 * 4 / THREADS;  // 16-byte loads per chunk
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes of one (chunk, point)
   static constexpr int CHUNKS = C / 16;
@@ -471,6 +486,49 @@ __device__ __forceinline__ void combine_k(f32x2 (&rk)[4], const f32x2 (&d)[8], f
   for (int b = 0; b < 4; ++b) rk[b] = pk_fma(fb, d[4 + b], pk_mul(fa, d[b]));
 }
 
+// Resident input (AZ_W4_RESIDENT): byte offset in X of (board bd, position pos, channel ch):
+// 16-channel chunk slots of 64 B, slot = chunk ^ ((column >> 1) & 3), so the four tiles of
+// a half-wave's window read (columns 2tx - 1 + b, tx = 0..3) hit four different bank groups
+template <class G>
+__device__ __forceinline__ int xoff(int bd, int pos, int ch) {
+  return (bd * 64 + pos) * (G::C * 4) + ((((ch >> 4) ^ (((pos & 7) >> 1) & 3)) << 6) | ((ch & 15) << 2));
+}
+
+// window rows of group KK for chunk c from X: xb[b] = the window's top-left row and column b
+// (unclamped: off-board entries read finite words, masked in combine_kx), chunk 0's slot
+template <class G, int KK>
+__device__ __forceinline__ void read_rows_x(f32x2 (&d)[8], const char* lds, const int (&xb)[4],
+                                            int c) {
+  constexpr int RB = 8 * G::C * 4;  // one board row
+  constexpr int o0 = G::XOFF + grp_a0(KK) * RB, o1 = G::XOFF + grp_a1(KK) * RB;
+  // opaque (an SGPR set here): with a compile-time chunk the compiler would otherwise hoist
+  // every peeled chunk's four addresses out of the layer loop (~50 live VGPRs, spills)
+  int xc = c << 6;
+  asm volatile("" : "+s"(xc));
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int a = xb[b] ^ xc;  // flips the chunk slot bits only
+    d[b] = *reinterpret_cast<const f32x2*>(lds + a + o0);
+    d[4 + b] = *reinterpret_cast<const f32x2*>(lds + a + o1);
+  }
+}
+
+// combine_k with the board-edge masks m = {top row valid, bottom row valid, left column valid,
+// right column valid} (0 / 1): a masked term is finite x 0, so the sums are the zero-padded
+// slot's (up to the sign of an exact zero)
+template <int KK>
+__device__ __forceinline__ void combine_kx(f32x2 (&rk)[4], const f32x2 (&d)[8], float vsc,
+                                           const float (&m)[4]) {
+  float fa_s = grp_sa(KK) * vsc, fb_s = grp_sb(KK) * vsc;
+  if constexpr (KK == 0) fa_s *= m[0];  // window row 2ty - 1
+  if constexpr (KK == 3) fb_s *= m[1];  // window row 2ty + 2
+  const f32x2 fa = {fa_s, fa_s}, fb = {fb_s, fb_s};
+#pragma unroll
+  for (int b = 0; b < 4; ++b) rk[b] = __builtin_elementwise_fma(fb, d[4 + b], fa * d[b]);
+  rk[0] = rk[0] * f32x2{m[2], m[2]};  // window column 2tx - 1
+  rk[3] = rk[3] * f32x2{m[3], m[3]};  // window column 2tx + 2
+}
+
 // a - b on an f32x2 as ONE v_pk_add_f32 with b negated: the compiler splits a two-wide
 // fsub into two v_sub_f32 (and folds an fma by -1 back into that fsub); same IEEE
 // differences element by element
@@ -601,6 +659,8 @@ struct St {
   int goff[G::LD_PER_THREAD], ldst[G::LD_PER_THREAD], rbase[G::TPT], cols[G::TPT], soff[G::TPT], aoff[G::NRT];
   float vsc[G::TPT];  // FP16X2: the item's board input scale 2^sv (1 otherwise)
   int cbase[G::TPT][4];  // AZ_W4_DIET: the item's window column bases in an input slot
+  int xb[G::TPT][4];     // AZ_W4_RESIDENT: the item's window bases in X (read_rows_x)
+  float xm[G::TPT][4];   // AZ_W4_RESIDENT: its board-edge masks (combine_kx)
   __amdgpu_buffer_rsrc_t rx, rw;  // input and weight descriptors (AZ_W4_DIET)
   int wlane, tid, b0, nb;
   int cs;             // first channel chunk of this workgroup's split (0 unless SPLIT)
@@ -670,14 +730,20 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // the chunk map at run time
 // TAIL (AZ_W4_TAIL): 1 = the layer's second-to-last chunk (its input-slice look-ahead is past
 // the end), 2 = the last (everything after its own MFMAs is)
-template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false, int TAIL = 0>
+// RSD (AZ_W4_RESIDENT): the layer input is resident in LDS -- no input-slice loads or stores,
+// the windows read from X, V buffer 1 after X
+template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false, int TAIL = 0,
+          bool RSD = false>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
-  constexpr bool NO_IN = TAIL >= 1, NO_NEXT = TAIL == 2;
+  static_assert(!RSD || CT, "the resident input needs the compile-time group rows");
+  constexpr bool NO_IN = TAIL >= 1 || RSD, NO_NEXT = TAIL == 2;
+  constexpr bool NO_WIN = TAIL >= 1;  // no window reads for chunk v + 2
+  constexpr int V1 = RSD ? G::V1R : G::BUF;
   W4C_STAMP(v, 0);
   const int L = lmap<G>(S, v);
-  const char* cur = S.lds + (v & 1) * G::BUF;
-  char* nxt = S.lds + ((v + 1) & 1) * G::BUF;
+  const char* cur = S.lds + (v & 1) * V1;
+  char* nxt = S.lds + ((v + 1) & 1) * V1;
   // chunk v+1's rows (its windows were requested during chunk v-1); the last chunk
   // transforms a clamped duplicate into the idle buffer (uniform body)
   const int Lr = lmap<G>(S, v + 1);
@@ -704,7 +770,9 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
       // behind step 0's MFMAs
 #pragma unroll
       for (int u = 0; u < G::TPT; ++u) {
-        if constexpr (CT)
+        if constexpr (RSD)
+          combine_kx<KR < 4 ? KR : 3>(S.rk[u], S.dr[u], S.vsc[u], S.xm[u]);
+        else if constexpr (CT)
           combine_k<KR < 4 ? KR : 3>(S.rk[u], S.dr[u], S.vsc[u]);
         else
           combine_rows(S.rk[u], S.dr[u], Lr);
@@ -718,7 +786,7 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     }
     // the chunk-after-next's input slice at the chunk's first step: four steps of latency
     // cover before it is stored to LDS at the chunk's end
-    if (l == 0 && !(AZ_W4_EXP & 2) && !NO_IN) {
+    if (l == 0 && !(AZ_W4_EXP & 2) && !(AZ_W4_EXP & 64) && !NO_IN) {
       if constexpr (AZ_W4_DIET)
         load_in<G>(S.ld[set_l], S.rx, S.goff, Ll);
       else
@@ -754,15 +822,17 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     __builtin_amdgcn_sched_barrier(0);
   }
   // slot (v+2) & 1 = v & 1 held chunk v's input, whose rows were formed in chunk v-1
-  if (!(AZ_W4_EXP & 2) && !NO_IN) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
+  if (!(AZ_W4_EXP & 2) && !(AZ_W4_EXP & 64) && !NO_IN) store_in<G>(S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.ld[set_s], S.ldst);
   W4C_STAMP(v, 1);
   if (!(AZ_W4_EXP & 8)) lds_barrier();
   W4C_STAMP(v, 2);
   if (!NO_NEXT) read_a<G>(S.af, nxt, 0, S.aoff);
   // the next chunk's window rows (chunk L+2, stored just before the barrier)
 #pragma unroll
-  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2) && !NO_IN; ++u) {
-    if constexpr (CT)
+  for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2) && !NO_WIN; ++u) {
+    if constexpr (RSD)
+      read_rows_x<G, KS < 4 ? KS : 3>(S.dr[u], S.lds, S.xb[u], Ls & 7);
+    else if constexpr (CT)
       read_rows_k<G, KS < 4 ? KS : 3, PAR>(S.dr[u], S.lds, S.cbase[u]);
     else
       read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
@@ -792,8 +862,9 @@ __device__ __forceinline__ void zero_acc(St<G>& S) {
 
 // transform-grid row K (compile time): its eight chunks (staging residual half STAGE, or
 // none for -1), then the fold
-template <class G, int K, int STAGE = -1>
+template <class G, int K, int STAGE = -1, bool RSD = false>
 __device__ __forceinline__ void run_group(St<G>& S) {
+  static_assert(!RSD || zero_free<G>(), "resident input: the zero-free whole-K kernel only");
   constexpr int KV = G::NG == 4 ? K : 0;  // the group's place in this workgroup's sequence
   if constexpr (G::NC == 1) {
     run_chunk<G, KV & 1, STAGE>(S, KV);  // one chunk per group: the parity alternates by group
@@ -803,16 +874,16 @@ __device__ __forceinline__ void run_group(St<G>& S) {
     // peeled so every group index is a compile-time constant; the first pair peeled too,
     // its first chunk's products starting the accumulators from C = 0
     constexpr int KN = K + 1;
-    run_chunk<G, 0, STAGE, K, K, true>(S, KV * G::NC);
-    run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + 1);
+    run_chunk<G, 0, STAGE, K, K, true, 0, RSD>(S, KV * G::NC);
+    run_chunk<G, 1, STAGE, K, K, false, 0, RSD>(S, KV * G::NC + 1);
 #pragma unroll 1
     for (int c = 2; c < G::NC - 2; c += 2) {
-      run_chunk<G, 0, STAGE, K, K>(S, KV * G::NC + c);
-      run_chunk<G, 1, STAGE, K, K>(S, KV * G::NC + c + 1);
+      run_chunk<G, 0, STAGE, K, K, false, 0, RSD>(S, KV * G::NC + c);
+      run_chunk<G, 1, STAGE, K, K, false, 0, RSD>(S, KV * G::NC + c + 1);
     }
     constexpr int T1 = AZ_W4_TAIL && K == 3 ? 1 : 0, T2 = AZ_W4_TAIL && K == 3 ? 2 : 0;
-    run_chunk<G, 0, STAGE, K, KN, false, T1>(S, KV * G::NC + G::NC - 2);
-    run_chunk<G, 1, STAGE, KN, KN, false, T2>(S, KV * G::NC + G::NC - 1);
+    run_chunk<G, 0, STAGE, K, KN, false, T1, RSD>(S, KV * G::NC + G::NC - 2);
+    run_chunk<G, 1, STAGE, KN, KN, false, T2, RSD>(S, KV * G::NC + G::NC - 1);
   } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
     constexpr int KN = K + 1;
 #pragma unroll 1
@@ -844,7 +915,11 @@ struct Epi {
 // output half I (rows 2ty + I): accumulator element e of row tile rt = tile 32rt + (e&3) +
 // 8(e>>2) + 4h, column co; Y[I][j] = output (2ty + I, 2tx + j); + bias (+ the staged
 // residual), ReLU, store, and the boards' max |y|
-template <class G, int I, bool RES, bool RELU, bool HEADS = false, bool KEEP = false>
+// RST: the residual is staged in LDS (else read from global memory); NOY: the output is not
+// stored to global memory (the resident trunk's conv1 outputs: only the next conv reads them,
+// from X)
+template <class G, int I, bool RES, bool RELU, bool HEADS = false, bool KEEP = false,
+          bool RST = G::RES_FITS, bool NOY = false>
 __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __restrict__ res,
                                          float* __restrict__ y, int rt0, int h) {
   constexpr int C = G::C;
@@ -859,7 +934,7 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
       // the output pair (2tx, 2tx + 1) of row 2ty + I shares its scale, bias and column: one
       // v_pk_fma_f32 for scale + bias (the power-of-two scaling is exact, so the fused form
       // rounds like the product then the sum), one packed residual add
-      if constexpr (!HEADS && G::SCALED && (!RES || G::RES_FITS)) {
+      if constexpr (!HEADS && G::SCALED && (!RES || RST)) {
         const float u = E.unsc[2 * t + (e >> 3)];
         f32x2 v = __builtin_elementwise_fma(f32x2{S.Y[I][0][t][e], S.Y[I][1][t][e]},
                                             f32x2{u, u}, f32x2{E.bv, E.bv});
@@ -873,8 +948,10 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
           v.y = fmaxf(v.y, 0.0f);
         }
         float* yp = &y[((size_t)(S.b0 + bd) * 64 + (2 * ty + I) * 8 + 2 * tx) * C + E.co];
-        yp[0] = v.x;
-        yp[C] = v.y;
+        if (!NOY && !((AZ_W4_EXP & 128) && !RES)) {
+          yp[0] = v.x;
+          yp[C] = v.y;
+        }
         if constexpr (KEEP) {
           S.Y[I][0][t][e] = v.x;
           S.Y[I][1][t][e] = v.y;
@@ -887,7 +964,7 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
       for (int j = 0; j < 2; ++j) {
         const int pos = (2 * ty + I) * 8 + 2 * tx + j;
         float v = (G::SCALED ? S.Y[I][j][t][e] * E.unsc[2 * t + (e >> 3)] : S.Y[I][j][t][e]) + E.bv;
-        if (RES && G::RES_FITS)
+        if (RES && RST)
           v += *reinterpret_cast<const float*>(
               S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx + j) * C + E.co) * 4);
         else if (RES)
@@ -896,7 +973,8 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
         if constexpr (HEADS) {  // kept for the fused heads (heads_epilogue), not stored
           S.Y[I][j][t][e] = v;
         } else {
-          if constexpr ((AZ_W4_NT & 2) != 0)
+          if constexpr (NOY) {
+          } else if constexpr ((AZ_W4_NT & 2) != 0)
             __builtin_nontemporal_store(v, &y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co]);
           else
             y[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co] = v;
@@ -971,8 +1049,15 @@ __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int
 // slices are already in the input slots and its per-board ranges in LDS (written by the
 // previous layer's HOUT epilogue, ordered by the layer fence); HOUT = write them for the next
 // layer.  Two-board, one-row-tile form only (the trunk's).
+// RSD (AZ_W4_RESIDENT, the persistent trunk's layers instead of the hand-off): the layer's whole
+// input is resident in LDS (X, G::XOFF) -- XFILL = load it from x first (a launch's first
+// conv), else the previous layer wrote it; XOUT = write this layer's output there after the
+// last window read (ordered by the layer fence).  No input slices are loaded or stored per
+// chunk; the residual is read from global memory in the epilogue (no LDS left to stage it);
+// a conv1 output with XOUT is not stored to global memory at all (only the next conv reads it).
 template <class G, bool RES, bool RELU, bool HEADS = false, bool LAUNDER = false,
-          bool HIN = false, bool HOUT = false>
+          bool HIN = false, bool HOUT = false, bool RSD = false, bool XFILL = false,
+          bool XOUT = false>
 __device__ __forceinline__ void conv_body(
     const float* __restrict__ x, const char* __restrict__ wq, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ y, int n_boards,
@@ -982,6 +1067,11 @@ __device__ __forceinline__ void conv_body(
   static_assert(!(HIN || HOUT) || (G::BOARDS == 2 && G::NRT == 1 && G::IPD == 1 && G::SCALED &&
                                    !G::SPLIT && LAUNDER),
                 "the layer hand-off is the persistent two-board fp16x2 trunk's");
+  static_assert(!(RSD || XFILL || XOUT) ||
+                    (RSD && !HIN && !HOUT && G::BOARDS == 2 && G::NRT == 1 && G::SCALED &&
+                     !G::SPLIT && LAUNDER && AZ_W4_DIET && C == 128),
+                "the resident input is the persistent two-board fp16x2 trunk's");
+  constexpr bool NOY = RSD && XOUT && !RES && !HEADS;
 
   extern __shared__ float4 lds4[];
   W4_STAMP(0);
@@ -1054,6 +1144,19 @@ __device__ __forceinline__ void conv_body(
       const int e = frexp_exp(bd < nb ? in_range(bd) : 0.0f);
       S.vsc[u] = ldexpf(1.0f, 13 - e);
     }
+    if constexpr (RSD) {
+      // X byte offset of the window's row 2ty - 1, column 2tx - 1 + b (chunk 0's slot; both
+      // may be off the board -- negative for the first board's top-left tile), channel pair p
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int col = 2 * tx - 1 + b;
+        S.xb[u][b] = (bd * 64 + (2 * ty - 1) * 8 + col) * (C * 4) + (((col >> 1) & 3) << 6) + p * 8;
+      }
+      S.xm[u][0] = ty == 0 ? 0.0f : 1.0f;
+      S.xm[u][1] = ty == 3 ? 0.0f : 1.0f;
+      S.xm[u][2] = tx == 0 ? 0.0f : 1.0f;
+      S.xm[u][3] = tx == 3 ? 0.0f : 1.0f;
+    }
   }
   // input loads: element e = j * THREADS + tid -> position P = e / 4 (board P / 64, clamped
   // to the last valid board: rows of absent boards are computed but never stored),
@@ -1075,7 +1178,44 @@ __device__ __forceinline__ void conv_body(
   // (the persistent trunk's later layers: the borders are still zero -- interior stores never
   // touch them -- and the layer fence ordered the previous layer's reads)
   const bool fill = !LAUNDER || layer == 0;
-  if constexpr (HIN) {
+  if constexpr (RSD) {
+    if constexpr (XFILL) {
+      // V buffers zeroed (a board-edge window reads some of their words: finite from here on),
+      // and the whole input into X: 16 loads of 16 bytes per thread, in two halves
+#pragma unroll
+      for (int i = tid * 16; i < G::BUF; i += G::THREADS * 16) {
+        *reinterpret_cast<f32x4*>(S.lds + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        *reinterpret_cast<f32x4*>(S.lds + G::V1R + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      int xst[G::LD_PER_THREAD];  // X offset of load element j in chunk 0's slot
+#pragma unroll
+      for (int j = 0; j < G::LD_PER_THREAD; ++j) {
+        const int e = j * G::THREADS + tid, P0 = e >> 2, q = e & 3;
+        const int P = (P0 & ~3) | ((P0 & 1) << 1) | ((P0 >> 1) & 1);
+        xst[j] = xoff<G>(P >> 6, P & 63, 4 * q);
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        f32x4 xl[4][G::LD_PER_THREAD];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) load_in<G>(xl[c], S.rx, S.goff, 4 * half + c);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int j = 0; j < G::LD_PER_THREAD; ++j)
+            *reinterpret_cast<f32x4*>(S.lds + G::XOFF + (xst[j] ^ ((4 * half + c) << 6))) = xl[c][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::PD; ++i) load_b<G>(S.bf[i], S.rw, S.wlane, qmap<G>(S, i));
+    if constexpr (XFILL) lds_barrier();  // X and the zeroed V buffers complete
+#pragma unroll
+    for (int u = 0; u < G::TPT; ++u) {
+      f32x2 d[8];
+      read_rows_x<G, 0>(d, S.lds, S.xb[u], 0);
+      combine_kx<0>(S.rk[u], d, S.vsc[u], S.xm[u]);
+    }
+  } else if constexpr (HIN) {
     // chunks 0 and 1 are in the slots already (the previous layer's hand-off, ordered by the
     // layer fence); chunk 2's slice (stored at the end of chunk 0) and the first weight steps
     char* in0 = S.lds + G::IN_OFF;
@@ -1118,18 +1258,23 @@ __device__ __forceinline__ void conv_body(
   }
 #pragma unroll
   for (int u = 0; u < G::TPT; ++u) {
-    put_point<G, 0>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
-    put_point<G, 1>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
-    put_point<G, 2>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
-    put_point<G, 3>(S.lds, S.rk[u], S.soff[u], S.vsc[u]);
+    const float vs = RSD ? 1.0f : S.vsc[u];  // RSD: the scale is in rk already
+    put_point<G, 0>(S.lds, S.rk[u], S.soff[u], vs);
+    put_point<G, 1>(S.lds, S.rk[u], S.soff[u], vs);
+    put_point<G, 2>(S.lds, S.rk[u], S.soff[u], vs);
+    put_point<G, 3>(S.lds, S.rk[u], S.soff[u], vs);
   }
   lds_barrier();
 
   if constexpr (!zero_free<G>()) zero_acc<G>(S);
   read_a<G>(S.af, S.lds, 0, S.aoff);
 #pragma unroll
-  for (int u = 0; u < G::TPT; ++u)
-    read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], S.cols[u], lmap<G>(S, 1));
+  for (int u = 0; u < G::TPT; ++u) {
+    if constexpr (RSD)
+      read_rows_x<G, 0>(S.dr[u], S.lds, S.xb[u], 1);
+    else
+      read_rows<G>(S.dr[u], S.lds + G::IN_OFF + G::IN_SLOT, S.rbase[u], S.cols[u], lmap<G>(S, 1));
+  }
   // epilogue constants: bias, and (FP16X2) the scale M carries, 2^(su + sv_board); removing
   // it is an exact power-of-two product
   Epi<G> E;
@@ -1172,23 +1317,45 @@ __device__ __forceinline__ void conv_body(
     epilogue<G, 1, false, false>(S, E, res, y, rt0, h);
     return;
   } else {
-  run_group<G, 0>(S);
+  run_group<G, 0, -1, RSD>(S);
   W4_STAMP(2);
-  run_group<G, 1>(S);
+  run_group<G, 1, -1, RSD>(S);
   W4_STAMP(3);
   // output rows 2ty (Y[0]) are final after group 2: stored while group 3 computes, with
   // their residual staged through LDS during group 2 (and the odd rows' during group 3)
-  constexpr bool STAGED = RES && G::RES_FITS && !G::SPLIT;
-  run_group<G, 2, STAGED ? 0 : -1>(S);
+  constexpr bool STAGED = RES && G::RES_FITS && !G::SPLIT && !RSD;
+  constexpr bool KEEPY = HOUT || XOUT;
+  run_group<G, 2, STAGED ? 0 : -1, RSD>(S);
   W4_STAMP(4);
   W4T_STAMP(layer, 2);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
-  epilogue<G, 0, RES, RELU, HEADS, HOUT>(S, E, res, y, rt0, h);
+  epilogue<G, 0, RES, RELU, HEADS, KEEPY, STAGED, NOY>(S, E, res, y, rt0, h);
   if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
-  run_group<G, 3, STAGED ? 1 : -1>(S);
+  run_group<G, 3, STAGED ? 1 : -1, RSD>(S);
   W4_STAMP(5);
   if (STAGED) vm_barrier();
-  epilogue<G, 1, RES, RELU, HEADS, HOUT>(S, E, res, y, rt0, h);
+  epilogue<G, 1, RES, RELU, HEADS, KEEPY, STAGED, NOY>(S, E, res, y, rt0, h);
+  if constexpr (XOUT) {
+    // the next layer's input, whole, into X: every window read of this layer's X was issued
+    // before the second-to-last chunk's barrier (the tail chunks read none) and completed
+    // before the last chunk's; the layer fence orders these stores before the next reads.
+    // Element e of half i: tile T = (e & 3) + 8 (e >> 2) + 4 h -> board e >> 3, tile column
+    // e & 3, tile row (2 (e >> 2) + h) & 3; column slot swizzle (2tx + j) >> 1 = tx
+    const int cpart = ((E.co >> 4) << 6) | ((E.co & 15) << 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int bd = e >> 3, tx = e & 3, ty = (2 * (e >> 2) + h) & 3;
+        if (bd >= nb) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int pos = (2 * ty + i) * 8 + 2 * tx + j;
+          *reinterpret_cast<float*>(S.lds + G::XOFF + (bd * 64 + pos) * (C * 4) +
+                                    (cpart ^ (tx << 6))) = S.Y[i][j][0][e];
+        }
+      }
+  }
   if constexpr (HOUT) {
     // the next layer's input: its first two slices (channels 0-31 = column block 0's
     // registers) into the input slots -- free since the last chunk's windows were read,
@@ -1408,6 +1575,56 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   const float* h = a.h_in;
   int ob = 0;
   const int n_loop = EPI ? a.n_convs - 1 : a.n_convs;
+  if constexpr (AZ_W4_RESIDENT) {
+    // the resident input: conv1 (even i) reads X, writes t only into X; conv2 reads t from X
+    // and the residual h from global memory, writes h to global memory (the next block's
+    // residual) and into X.  A launch's first conv loads X; its last writes none
+    for (int i = 0; i < n_loop; ++i) {
+      if (i > 0) layer_fence();
+      const bool xout = i + 1 < a.n_convs;
+      if ((i & 1) == 0) {
+        if (i == 0 && xout)
+          conv_body<G, false, true, false, true, false, false, true, true, true>(
+              h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards,
+              a.amax[0], a.amax[1], HeadsOut{}, i);
+        else if (i == 0)
+          conv_body<G, false, true, false, true, false, false, true, true, false>(
+              h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards,
+              a.amax[0], a.amax[1], HeadsOut{}, i);
+        else if (xout)
+          conv_body<G, false, true, false, true, false, false, true, false, true>(
+              h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards,
+              a.amax[0], a.amax[1], HeadsOut{}, i);
+        else
+          conv_body<G, false, true, false, true, false, false, true, false, false>(
+              h, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), nullptr, a.t, a.n_boards,
+              a.amax[0], a.amax[1], HeadsOut{}, i);
+      } else {
+        const bool last_heads = HEADS && i == a.n_convs - 1;
+        if (xout)
+          conv_body<G, true, true, false, true, false, false, true, false, true>(
+              a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h, a.hb[ob], a.n_boards,
+              a.amax[1], last_heads ? nullptr : a.amax[0], HeadsOut{}, i);
+        else
+          conv_body<G, true, true, false, true, false, false, true, false, false>(
+              a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h, a.hb[ob], a.n_boards,
+              a.amax[1], last_heads ? nullptr : a.amax[0], HeadsOut{}, i);
+        h = a.hb[ob];
+        ob ^= 1;
+      }
+    }
+    if constexpr (EPI) {
+      layer_fence();  // the last block's conv1 output in X, ordered for this workgroup
+      const int i = a.n_convs - 1;
+      conv_body<G, true, true, true, true, false, false, true, false, false>(
+          a.t, uniform_ptr(a.wq[i]), uniform_ptr(a.bias[i]), h, nullptr, a.n_boards, a.amax[1],
+          nullptr, ho, i);
+    } else if constexpr (HEADS) {
+      layer_fence();
+      trunk_heads<G>(h, a.n_boards, ho);
+    }
+    return;
+  }
   constexpr bool HO = AZ_W4_HANDOFF != 0;
   for (int i = 0; i < n_loop; ++i) {
     if (i > 0) layer_fence();
@@ -1707,13 +1924,13 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::TRUNK_LDS));
     attr_set = true;
   }
   const TrunkW4 a{reinterpret_cast<const char* const*>(wq), bias, h_in, {hb0, hb1}, t,
                   {amax0, amax1}, planes, stem_w, stem_b, n_boards, n_convs};
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
-  hipLaunchKernelGGL((k_trunk_wino4<G>), dim3(grid), dim3(G::THREADS), (size_t)G::LDS_BYTES,
+  hipLaunchKernelGGL((k_trunk_wino4<G>), dim3(grid), dim3(G::THREADS), (size_t)G::TRUNK_LDS,
                      azc::as_stream(stream), a, HeadsOut{});
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -1753,7 +1970,7 @@ extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* cons
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G, true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS_BYTES));
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::TRUNK_LDS));
     attr_set = true;
   }
   const TrunkW4 a{reinterpret_cast<const char* const*>(wq), bias, h_in, {hb0, hb1}, t,
@@ -1761,7 +1978,7 @@ extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* cons
   const HeadsOut ho{{wpv, bpv, wpolT, bpol, w1T, b1, w2, b2}, priors, values};
   const unsigned grid = (unsigned)((n_boards + G::BOARDS - 1) / G::BOARDS);
   hipLaunchKernelGGL((k_trunk_wino4<G, true>), dim3(grid), dim3(G::THREADS),
-                     (size_t)G::LDS_BYTES, azc::as_stream(stream), a, ho);
+                     (size_t)G::TRUNK_LDS, azc::as_stream(stream), a, ho);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -188,4 +188,36 @@ c10() {
   exit 0
 }
 
+c11() {
+  # upper bounds for a layer-resident input (wrong results): no in-loop input-slice loads /
+  # LDS stores (EXP 64), no global stores of conv1 outputs (EXP 128), both (EXP 192)
+  export OUT=gpurun_out/r05k
+  mkdir -p $OUT
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    for v in x64 x128 x192; do
+      run net_$v 120 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python scripts/net_time.py 1024 40
+    done
+  done
+  exit 0
+}
+
+c12() {
+  # the layer input resident in LDS (AZ_W4_RESIDENT=1): the trunk / heads bit-identity tests and
+  # the reference fixtures, then timed against the product alternately
+  export OUT=gpurun_out/r05l
+  mkdir -p $OUT
+  run rsd_tests 400 env AZ_LIB_PATH=expbuild/rsd/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread -k "persistent or trunk_heads or golden or matches or two_board" \
+    || exit $?
+  for i in 1 2 3; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    run net_rsd 120 env AZ_LIB_PATH=expbuild/rsd/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  run bench_tree 300 python bench.py --skip-cpu --skip-kernel
+  run bench_rsd 300 env AZ_LIB_PATH=expbuild/rsd/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+  exit 0
+}
+
 "$@"
