@@ -115,10 +115,12 @@
 #ifndef AZ_W4_TAIL
 #define AZ_W4_TAIL 1
 #endif
-// the persistent trunk's layer input resident in LDS (see conv_body): 0 = the per-chunk input
-// slices (A/B builds)
+// the persistent trunk's layer input resident in LDS (see conv_body): 416.2-417.1 -> 368.7-371.3
+// us per B = 1,024 trunk + heads launch, configs[2] bench 104.1 -> 116.7 games/s, same box,
+// outputs bit-identical (profiles/r05_resident_ab.json); 0 = the per-chunk input slices with
+// the two-slice hand-off (AZ_W4_HANDOFF)
 #ifndef AZ_W4_RESIDENT
-#define AZ_W4_RESIDENT 0
+#define AZ_W4_RESIDENT 1
 #endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
 // the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
