@@ -69,7 +69,8 @@
 // 8 = no LDS barrier in the loop, 16 = no A-fragment LDS reads, 32 = weight loads by the
 // first row tile's waves only (the other half reuses stale fragments), 64 = no input-slice
 // loads / LDS stores in the loop (the windows read stale slots), 128 = no global stores of a
-// non-residual conv's output.  Product: 0.
+// non-residual conv's output, 256 = no global residual reads (the resident trunk's RES
+// epilogues), 512 = no resident-input write-out.  Product: 0.
 #ifndef AZ_W4_EXP
 #define AZ_W4_EXP 0
 #endif
@@ -969,7 +970,7 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
         if (RES && RST)
           v += *reinterpret_cast<const float*>(
               S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx + j) * C + E.co) * 4);
-        else if (RES)
+        else if (RES && !(AZ_W4_EXP & 256))
           v += res[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co];
         if (RELU) v = fmaxf(v, 0.0f);
         if constexpr (HEADS) {  // kept for the fused heads (heads_epilogue), not stored
@@ -1337,7 +1338,7 @@ __device__ __forceinline__ void conv_body(
   W4_STAMP(5);
   if (STAGED) vm_barrier();
   epilogue<G, 1, RES, RELU, HEADS, KEEPY, STAGED, NOY>(S, E, res, y, rt0, h);
-  if constexpr (XOUT) {
+  if constexpr (XOUT && !(AZ_W4_EXP & 512)) {
     // the next layer's input, whole, into X: every window read of this layer's X was issued
     // before the second-to-last chunk's barrier (the tail chunks read none) and completed
     // before the last chunk's; the layer fence orders these stores before the next reads.

@@ -220,4 +220,18 @@ c12() {
   exit 0
 }
 
+c13() {
+  # what the resident trunk still pays (wrong-result builds): the RES epilogues' global residual
+  # reads (EXP 256), the X write-out (EXP 512)
+  export OUT=gpurun_out/r05m
+  mkdir -p $OUT
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    for v in x256 x512; do
+      run net_$v 120 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python scripts/net_time.py 1024 40
+    done
+  done
+  exit 0
+}
+
 "$@"
