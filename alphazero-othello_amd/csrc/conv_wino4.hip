@@ -123,6 +123,12 @@
 #ifndef AZ_W4_RESIDENT
 #define AZ_W4_RESIDENT 1
 #endif
+// with the resident input: a residual conv stages its residual rows in X's odd rows, free
+// while the transform-grid row 3 (even input rows only) runs -- half 0 from the end of
+// group 2's seventh chunk, half 1 during group 3; 0 = read from global memory in the epilogue
+#ifndef AZ_W4_RXS
+#define AZ_W4_RXS 0
+#endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
 // the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
 // + heads launch, same box (profiles/r05_conv_micro_ab.json); 0 = one element at a time
@@ -725,6 +731,17 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
   }
 }
 
+// the resident trunk's residual staging (AZ_W4_RXS): segment c = (board c / 4, ty = c % 4) of
+// half I -- row 2ty + I of the board, 8 positions x C fp32 = 4 KiB, one 16-byte piece per
+// thread -- into X's row 2ty + 1 of that board (linear [8][C]); S.lds_res = X + 1 KiB x wave
+template <class G, int I>
+__device__ __forceinline__ void res_dma_x(St<G>& S, int c) {
+  static_assert(G::THREADS * 16 == 8 * G::C * 4, "one 4 KiB row segment per workgroup pass");
+  const int bd = c >> 2, ty = c & 3, bs = bd < S.nb ? bd : S.nb - 1;
+  glds16(S.res + ((size_t)(S.b0 + bs) * 64 + (2 * ty + I) * 8) * G::C + 4 * S.tid,
+         __builtin_amdgcn_readfirstlane(S.lds_res + (bd * 64 + (2 * ty + 1) * 8) * G::C * 4));
+}
+
 // one chunk L (of parity PAR, so a step's weight ring slot is a compile-time constant): its
 // four steps, the next chunk's transform into the other LDS buffer, the windows of the
 // chunk after that requested
@@ -735,8 +752,11 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // the end), 2 = the last (everything after its own MFMAs is)
 // RSD (AZ_W4_RESIDENT): the layer input is resident in LDS -- no input-slice loads or stores,
 // the windows read from X, V buffer 1 after X
+// RDMA >= 0 (the resident trunk's residual staging): after this chunk's window reads, every
+// segment of residual half RDMA into X's odd rows (no window reads them from here to the
+// layer's end)
 template <class G, int PAR, int STAGE, int KR = -1, int KS = -1, bool FIRST = false, int TAIL = 0,
-          bool RSD = false>
+          bool RSD = false, int RDMA = -1>
 __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
   constexpr bool CT = AZ_W4_DIET && KR >= 0 && KS >= 0;
   static_assert(!RSD || CT, "the resident input needs the compile-time group rows");
@@ -796,7 +816,11 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
         load_in<G>(S.ld[set_l], S.x, S.goff, Ll);
     }
     if constexpr (STAGE >= 0) {
-      if (l == 1) res_dma<G, STAGE>(S, L & 7);
+      if constexpr (RSD) {
+        if (l == 1) res_dma_x<G, STAGE>(S, L & 7);
+      } else {
+        if (l == 1) res_dma<G, STAGE>(S, L & 7);
+      }
     }
 #pragma unroll
     for (int u = 0; u < G::TPT && !(AZ_W4_EXP & 2) && !NO_NEXT; ++u) {
@@ -840,6 +864,10 @@ __device__ __forceinline__ void run_chunk(St<G>& S, int v) {
     else
       read_rows<G>(S.dr[u], S.lds + G::IN_OFF + (v & 1) * G::IN_SLOT, S.rbase[u], S.cols[u], Ls);
   }
+  if constexpr (RDMA >= 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) res_dma_x<G, RDMA>(S, c);
+  }
 }
 
 // groups whose first chunk starts the accumulators itself (mma<G, true>): the whole-K
@@ -865,7 +893,7 @@ __device__ __forceinline__ void zero_acc(St<G>& S) {
 
 // transform-grid row K (compile time): its eight chunks (staging residual half STAGE, or
 // none for -1), then the fold
-template <class G, int K, int STAGE = -1, bool RSD = false>
+template <class G, int K, int STAGE = -1, bool RSD = false, int RDMA = -1>
 __device__ __forceinline__ void run_group(St<G>& S) {
   static_assert(!RSD || zero_free<G>(), "resident input: the zero-free whole-K kernel only");
   constexpr int KV = G::NG == 4 ? K : 0;  // the group's place in this workgroup's sequence
@@ -885,7 +913,7 @@ __device__ __forceinline__ void run_group(St<G>& S) {
       run_chunk<G, 1, STAGE, K, K, false, 0, RSD>(S, KV * G::NC + c + 1);
     }
     constexpr int T1 = AZ_W4_TAIL && K == 3 ? 1 : 0, T2 = AZ_W4_TAIL && K == 3 ? 2 : 0;
-    run_chunk<G, 0, STAGE, K, KN, false, T1, RSD>(S, KV * G::NC + G::NC - 2);
+    run_chunk<G, 0, STAGE, K, KN, false, T1, RSD, RDMA>(S, KV * G::NC + G::NC - 2);
     run_chunk<G, 1, STAGE, KN, KN, false, T2, RSD>(S, KV * G::NC + G::NC - 1);
   } else if constexpr (AZ_W4_DIET && !G::SPLIT) {
     constexpr int KN = K + 1;
@@ -922,7 +950,7 @@ struct Epi {
 // stored to global memory (the resident trunk's conv1 outputs: only the next conv reads them,
 // from X)
 template <class G, int I, bool RES, bool RELU, bool HEADS = false, bool KEEP = false,
-          bool RST = G::RES_FITS, bool NOY = false>
+          bool RST = G::RES_FITS, bool NOY = false, bool RXS = false>
 __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __restrict__ res,
                                          float* __restrict__ y, int rt0, int h) {
   constexpr int C = G::C;
@@ -943,7 +971,8 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
                                             f32x2{u, u}, f32x2{E.bv, E.bv});
         if constexpr (RES) {
           const float* rp = reinterpret_cast<const float*>(
-              S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx) * C + E.co) * 4);
+              RXS ? S.lds + G::XOFF + ((bd * 64 + (2 * ty + 1) * 8 + 2 * tx) * C + E.co) * 4
+                  : S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx) * C + E.co) * 4);
           v = v + f32x2{rp[0], rp[C]};
         }
         if (RELU) {
@@ -969,7 +998,8 @@ __device__ __forceinline__ void epilogue(St<G>& S, Epi<G>& E, const float* __res
         float v = (G::SCALED ? S.Y[I][j][t][e] * E.unsc[2 * t + (e >> 3)] : S.Y[I][j][t][e]) + E.bv;
         if (RES && RST)
           v += *reinterpret_cast<const float*>(
-              S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx + j) * C + E.co) * 4);
+              RXS ? S.lds + G::XOFF + ((bd * 64 + (2 * ty + 1) * 8 + 2 * tx + j) * C + E.co) * 4
+                  : S.lds + G::RES_OFF + (((bd * 4 + ty) * 8 + 2 * tx + j) * C + E.co) * 4);
         else if (RES && !(AZ_W4_EXP & 256))
           v += res[((size_t)(S.b0 + bd) * 64 + pos) * C + E.co];
         if (RELU) v = fmaxf(v, 0.0f);
@@ -1120,7 +1150,7 @@ __device__ __forceinline__ void conv_body(
   S.cs = G::SPLIT ? (int)(blockIdx.y % (G::CHUNKS / G::NC)) * G::NC : 0;
   S.g0 = G::NG == 1 ? (int)(blockIdx.y / (G::CHUNKS / G::NC)) : 0;
   if constexpr (G::SPLIT) y += (size_t)blockIdx.y * n_boards * 64 * C;  // this split's partials
-  S.lds_res = (unsigned)(uintptr_t)(S.lds + G::RES_OFF) + 16 * 64 * wave;
+  S.lds_res = (unsigned)(uintptr_t)(S.lds + (RSD ? G::XOFF : G::RES_OFF)) + 16 * 64 * wave;
   S.wlane = (col0 + r) * 32 + h * 16;
 #pragma unroll
   for (int t = 0; t < G::NRT; ++t)
@@ -1326,18 +1356,21 @@ __device__ __forceinline__ void conv_body(
   W4_STAMP(3);
   // output rows 2ty (Y[0]) are final after group 2: stored while group 3 computes, with
   // their residual staged through LDS during group 2 (and the odd rows' during group 3)
-  constexpr bool STAGED = RES && G::RES_FITS && !G::SPLIT && !RSD;
+  // the resident trunk stages its residual in X's odd rows instead (AZ_W4_RXS)
+  constexpr bool SX = RSD && RES && AZ_W4_RXS;
+  constexpr bool STAGED = (RES && G::RES_FITS && !G::SPLIT && !RSD) || SX;
   constexpr bool KEEPY = HOUT || XOUT;
-  run_group<G, 2, STAGED ? 0 : -1, RSD>(S);
+  run_group<G, 2, STAGED && !SX ? 0 : -1, RSD, SX ? 0 : -1>(S);
   W4_STAMP(4);
   W4T_STAMP(layer, 2);
   if (STAGED) vm_barrier();  // the even-row residual has landed in LDS
-  epilogue<G, 0, RES, RELU, HEADS, KEEPY, STAGED, NOY>(S, E, res, y, rt0, h);
+  epilogue<G, 0, RES, RELU, HEADS, KEEPY, STAGED, NOY, SX>(S, E, res, y, rt0, h);
   if (STAGED) lds_barrier();  // every wave's even-row residual reads before the odd rows land
   run_group<G, 3, STAGED ? 1 : -1, RSD>(S);
   W4_STAMP(5);
   if (STAGED) vm_barrier();
-  epilogue<G, 1, RES, RELU, HEADS, KEEPY, STAGED, NOY>(S, E, res, y, rt0, h);
+  epilogue<G, 1, RES, RELU, HEADS, KEEPY, STAGED, NOY, SX>(S, E, res, y, rt0, h);
+  if constexpr (SX && XOUT) lds_barrier();  // every wave's odd-row residual reads, then X rewritten
   if constexpr (XOUT && !(AZ_W4_EXP & 512)) {
     // the next layer's input, whole, into X: every window read of this layer's X was issued
     // before the second-to-last chunk's barrier (the tail chunks read none) and completed

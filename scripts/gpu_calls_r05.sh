@@ -234,4 +234,22 @@ c13() {
   exit 0
 }
 
+c14() {
+  # the resident trunk's residual staged in X's odd rows (AZ_W4_RXS=1): trunk / heads tests,
+  # then timed against the product alternately, and the bench
+  export OUT=gpurun_out/r05n
+  mkdir -p $OUT
+  run rxs_tests 400 env AZ_LIB_PATH=expbuild/rxs/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread -k "persistent or trunk_heads or golden or matches or two_board" \
+    || exit $?
+  for i in 1 2 3; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    run net_rxs 120 env AZ_LIB_PATH=expbuild/rxs/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  run bench_tree 300 python bench.py --skip-cpu --skip-kernel
+  run bench_rxs 300 env AZ_LIB_PATH=expbuild/rxs/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+  exit 0
+}
+
 "$@"
