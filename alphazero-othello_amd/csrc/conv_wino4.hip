@@ -125,9 +125,11 @@
 #endif
 // with the resident input: a residual conv stages its residual rows in X's odd rows, free
 // while the transform-grid row 3 (even input rows only) runs -- half 0 from the end of
-// group 2's seventh chunk, half 1 during group 3; 0 = read from global memory in the epilogue
+// group 2's seventh chunk, half 1 during group 3: 374.9-376.2 -> 344.4-345.9 us per B = 1,024
+// trunk + heads launch, configs[2] 116.9 -> 124.5 games/s, same box, bit-identical
+// (profiles/r05_resident_ab.json); 0 = read from global memory in the epilogue
 #ifndef AZ_W4_RXS
-#define AZ_W4_RXS 0
+#define AZ_W4_RXS 1
 #endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
 // the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
