@@ -252,4 +252,31 @@ c14() {
   exit 0
 }
 
+c15() {
+  # the final tree (resident trunk + residual staging): the whole GPU suite, smoke(), the bench
+  # line, a graph-mode kernel trace, the trunk's SQ / TA / L2 counters
+  export OUT=gpurun_out/r05o
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench 600 python bench.py
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_graph 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof -o run -- python3 bench.py --skip-cpu --steps 400 --warmup 2000
+  unset DEBUG_CLR_GRAPH_PACKET_CAPTURE
+  i=0
+  for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC" \
+             "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU" \
+             "GRBM_GUI_ACTIVE GRBM_COUNT TA_BUSY_avr TA_TA_BUSY_sum" \
+             "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_VMEM SQ_VALU_MFMA_COEXEC_CYCLES" \
+             "FETCH_SIZE" "WRITE_SIZE" \
+             "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
+    i=$((i+1))
+    run sq_trunk_$i 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq_trunk_$i -o pmc -- \
+      python3 scripts/trunk_one.py 1024 20 calib || exit $?
+  done
+  exit 0
+}
+
 "$@"
