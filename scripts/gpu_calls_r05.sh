@@ -279,4 +279,31 @@ c15() {
   exit 0
 }
 
+c16() {
+  # what binds the resident trunk now (wrong-result builds): no weight loads (EXP 1), no
+  # transform / window work (EXP 2), no MFMAs (EXP 4), no chunk barrier (EXP 8)
+  export OUT=gpurun_out/r05p
+  mkdir -p $OUT
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    for v in e1 e2 e4 e8; do
+      run net_$v 120 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python scripts/net_time.py 1024 40
+    done
+  done
+  exit 0
+}
+
+c17() {
+  # the resident trunk's sensitivity to the weight prefetch distance (AZ_W4_PD3 = 3 default)
+  export OUT=gpurun_out/r05q
+  mkdir -p $OUT
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    for v in pd2 pd1; do
+      run net_$v 120 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python scripts/net_time.py 1024 40
+    done
+  done
+  exit 0
+}
+
 "$@"
