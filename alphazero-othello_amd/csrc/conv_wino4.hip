@@ -131,6 +131,12 @@
 #ifndef AZ_W4_RXS
 #define AZ_W4_RXS 1
 #endif
+// boards per workgroup of the persistent trunk (az_trunk_wino4_gpu / _heads_gpu): 2 = two
+// workgroups per CU; 4 = one eight-wave workgroup per CU (with the resident input: X 128 KiB +
+// two 16 KiB V buffers = all 160 KiB), half the weight stream per board (A/B builds)
+#ifndef AZ_W4_TRUNK_BOARDS
+#define AZ_W4_TRUNK_BOARDS 2
+#endif
 // the epilogue's output pairs (2tx, 2tx + 1) as packed f32x2 (scale + bias in one v_pk_fma_f32,
 // the staged residual in one packed add): 411.0-411.5 -> 409.0-410.3 us per B = 1,024 trunk
 // + heads launch, same box (profiles/r05_conv_micro_ab.json); 0 = one element at a time
@@ -738,9 +744,13 @@ __device__ __forceinline__ void res_dma(St<G>& S, int c) {
 // thread -- into X's row 2ty + 1 of that board (linear [8][C]); S.lds_res = X + 1 KiB x wave
 template <class G, int I>
 __device__ __forceinline__ void res_dma_x(St<G>& S, int c) {
-  static_assert(G::THREADS * 16 == 8 * G::C * 4, "one 4 KiB row segment per workgroup pass");
-  const int bd = c >> 2, ty = c & 3, bs = bd < S.nb ? bd : S.nb - 1;
-  glds16(S.res + ((size_t)(S.b0 + bs) * 64 + (2 * ty + I) * 8) * G::C + 4 * S.tid,
+  // pass c of 8: segments c * SP .. c * SP + SP - 1 (SP = 1 with 256 threads, 2 with 512),
+  // 256 threads per 4 KiB segment
+  constexpr int SP = G::THREADS / 256;
+  static_assert(SP * 8 == G::BOARDS * 4, "eight passes per residual half");
+  const int seg = c * SP + (S.tid >> 8);
+  const int bd = seg >> 2, ty = seg & 3, bs = bd < S.nb ? bd : S.nb - 1;
+  glds16(S.res + ((size_t)(S.b0 + bs) * 64 + (2 * ty + I) * 8) * G::C + 4 * (S.tid & 255),
          __builtin_amdgcn_readfirstlane(S.lds_res + (bd * 64 + (2 * ty + 1) * 8) * G::C * 4));
 }
 
@@ -1103,7 +1113,8 @@ __device__ __forceinline__ void conv_body(
                                    !G::SPLIT && LAUNDER),
                 "the layer hand-off is the persistent two-board fp16x2 trunk's");
   static_assert(!(RSD || XFILL || XOUT) ||
-                    (RSD && !HIN && !HOUT && G::BOARDS == 2 && G::NRT == 1 && G::SCALED &&
+                    (RSD && !HIN && !HOUT && (G::BOARDS == 2 || G::BOARDS == 4) && G::NRT == 1 &&
+                     G::SCALED &&
                      !G::SPLIT && LAUNDER && AZ_W4_DIET && C == 128),
                 "the resident input is the persistent two-board fp16x2 trunk's");
   constexpr bool NOY = RSD && XOUT && !RES && !HEADS;
@@ -1152,7 +1163,8 @@ __device__ __forceinline__ void conv_body(
   S.cs = G::SPLIT ? (int)(blockIdx.y % (G::CHUNKS / G::NC)) * G::NC : 0;
   S.g0 = G::NG == 1 ? (int)(blockIdx.y / (G::CHUNKS / G::NC)) : 0;
   if constexpr (G::SPLIT) y += (size_t)blockIdx.y * n_boards * 64 * C;  // this split's partials
-  S.lds_res = (unsigned)(uintptr_t)(S.lds + (RSD ? G::XOFF : G::RES_OFF)) + 16 * 64 * wave;
+  S.lds_res = (unsigned)(uintptr_t)(S.lds + (RSD ? G::XOFF : G::RES_OFF)) +
+              16 * 64 * (RSD ? (wave & 3) : wave);
   S.wlane = (col0 + r) * 32 + h * 16;
 #pragma unroll
   for (int t = 0; t < G::NRT; ++t)
@@ -1377,14 +1389,14 @@ __device__ __forceinline__ void conv_body(
     // the next layer's input, whole, into X: every window read of this layer's X was issued
     // before the second-to-last chunk's barrier (the tail chunks read none) and completed
     // before the last chunk's; the layer fence orders these stores before the next reads.
-    // Element e of half i: tile T = (e & 3) + 8 (e >> 2) + 4 h -> board e >> 3, tile column
+    // Element e of half i: tile T = 32 rt0 + (e & 3) + 8 (e >> 2) + 4 h -> board 2 rt0 + (e >> 3), tile column
     // e & 3, tile row (2 (e >> 2) + h) & 3; column slot swizzle (2tx + j) >> 1 = tx
     const int cpart = ((E.co >> 4) << 6) | ((E.co & 15) << 2);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int bd = e >> 3, tx = e & 3, ty = (2 * (e >> 2) + h) & 3;
+        const int bd = 2 * rt0 + (e >> 3), tx = e & 3, ty = (2 * (e >> 2) + h) & 3;
         if (bd >= nb) continue;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1507,6 +1519,7 @@ __device__ __forceinline__ void stem_board(const float* __restrict__ planes,
                                            float* s_max) {
   constexpr int CO = 128, G4 = CO / 4, PPI = 256 / G4;
   const int tid = threadIdx.x;
+  const bool act = tid < 256;  // threads 256.. of a 512-thread workgroup only meet the barriers
   const int co = (tid % G4) * 4;
   float4 wv[9];
 #pragma unroll
@@ -1518,7 +1531,7 @@ __device__ __forceinline__ void stem_board(const float* __restrict__ planes,
   float4* out = reinterpret_cast<float4*>(y + (size_t)b * 64 * CO);
   float bmax = 0.0f;
 #pragma unroll
-  for (int p0 = 0; p0 < 64; p0 += PPI) {
+  for (int p0 = 0; p0 < 64 && act; p0 += PPI) {
     const int p = p0 + tid / G4, py = p >> 3, px = p & 7;
     float4 acc = bv;
 #pragma unroll
@@ -1541,7 +1554,7 @@ __device__ __forceinline__ void stem_board(const float* __restrict__ planes,
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, off, 64));
-  if ((tid & 63) == 0) s_max[tid >> 6] = bmax;
+  if ((tid & 63) == 0 && act) s_max[tid >> 6] = bmax;
   __syncthreads();
   if (tid == 0) absmax[b] = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
 }
@@ -1602,7 +1615,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
   }
 #endif
   if (a.planes) {  // the stem of this workgroup's boards first (its output never leaves L2)
-    static_assert(G::THREADS == 256 && G::C == 128, "stem_board's mapping");
+    static_assert(G::THREADS >= 256 && G::C == 128, "stem_board's mapping");
     extern __shared__ float4 lds4[];
     float* sp = reinterpret_cast<float*>(lds4);
     const int b0 = blockIdx.x * G::BOARDS;
@@ -1663,7 +1676,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
     }
     return;
   }
-  constexpr bool HO = AZ_W4_HANDOFF != 0;
+  constexpr bool HO = AZ_W4_HANDOFF != 0 && G::BOARDS == 2;  // the hand-off: two-board only
   for (int i = 0; i < n_loop; ++i) {
     if (i > 0) layer_fence();
     // a conv whose output the next conv reads hands it off through LDS (every conv but the
@@ -1958,7 +1971,7 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
              channels);
   AZ_REQUIRE(!planes || (stem_w && stem_b && ((uintptr_t)stem_w | (uintptr_t)stem_b) % 16 == 0),
              AZ_ERR_ARG, "az_trunk_wino4_gpu: planes without 16-byte aligned stem weights");
-  using G = W4<AZ_CONV_FP16X2, 1, 2>;  // two-board workgroups, FP16X2
+  using G = W4<AZ_CONV_FP16X2, 1, AZ_W4_TRUNK_BOARDS>;  // two-board workgroups, FP16X2
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G>,
@@ -2004,7 +2017,7 @@ extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* cons
              AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: null heads buffer");
   AZ_REQUIRE(((uintptr_t)wpv | (uintptr_t)w1T | (uintptr_t)b1 | (uintptr_t)w2) % 16 == 0,
              AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: heads weights must be 16-byte aligned");
-  using G = W4<AZ_CONV_FP16X2, 1, 2>;  // two-board workgroups, FP16X2
+  using G = W4<AZ_CONV_FP16X2, 1, AZ_W4_TRUNK_BOARDS>;  // two-board workgroups, FP16X2
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G, true>,

@@ -306,4 +306,22 @@ c17() {
   exit 0
 }
 
+c18() {
+  # the resident trunk in four-board eight-wave workgroups, one per CU (AZ_W4_TRUNK_BOARDS=4):
+  # trunk / heads tests, then timed against the product alternately, and the bench
+  export OUT=gpurun_out/r05r
+  mkdir -p $OUT
+  run tb4_tests 400 env AZ_LIB_PATH=expbuild/tb4/libaz_othello.so python -u -m pytest \
+    tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread -k "persistent or trunk_heads or golden or matches or two_board" \
+    || exit $?
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    run net_tb4 120 env AZ_LIB_PATH=expbuild/tb4/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  run bench_tree 300 python bench.py --skip-cpu --skip-kernel
+  run bench_tb4 300 env AZ_LIB_PATH=expbuild/tb4/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+  exit 0
+}
+
 "$@"
