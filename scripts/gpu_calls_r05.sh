@@ -324,4 +324,15 @@ c18() {
   exit 0
 }
 
+c19() {
+  # the other workloads on the final (resident-trunk) library
+  export OUT=gpurun_out/r05s
+  mkdir -p $OUT
+  run c2 500 python bench.py --workload c2 --skip-cpu --skip-kernel
+  run c4 500 python bench.py --workload c4 --skip-cpu --skip-kernel
+  run c5 500 python bench.py --workload c5 --skip-cpu --skip-kernel
+  run arena 600 python bench.py --workload arena --matches 1024
+  exit 0
+}
+
 "$@"
