@@ -335,4 +335,18 @@ c19() {
   exit 0
 }
 
+c20() {
+  # the select launch's level budget (AZ_SEL_LEVELS, 14 since round 3) re-tuned with the
+  # faster trunk: configs[2] bench lines alternated on one box
+  export OUT=gpurun_out/r05t
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_tree 300 python bench.py --skip-cpu --skip-kernel
+    for v in lv10 lv12 lv18; do
+      run bench_$v 300 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+    done
+  done
+  exit 0
+}
+
 "$@"
