@@ -522,11 +522,16 @@ __device__ __forceinline__ void read_rows_x(f32x2 (&d)[8], const char* lds, cons
   // every peeled chunk's four addresses out of the layer loop (~50 live VGPRs, spills)
   int xc = c << 6;
   asm volatile("" : "+s"(xc));
+  // the address as an LDS address, not as lds + offset: the dynamic LDS of the kernels using
+  // this (k_trunk_wino4: no static LDS, tests/test_isa_scan_cpu.py checks) starts at address
+  // 0, and the symbol's add of 0 cost one VALU per read pair
+  (void)lds;
+  typedef __attribute__((address_space(3))) const f32x2 lf32x2;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    const int a = xb[b] ^ xc;  // flips the chunk slot bits only
-    d[b] = *reinterpret_cast<const f32x2*>(lds + a + o0);
-    d[4 + b] = *reinterpret_cast<const f32x2*>(lds + a + o1);
+    const unsigned a = (unsigned)(xb[b] ^ xc);  // flips the chunk slot bits only
+    d[b] = *reinterpret_cast<lf32x2*>((size_t)(a + o0));
+    d[4 + b] = *reinterpret_cast<lf32x2*>((size_t)(a + o1));
   }
 }
 

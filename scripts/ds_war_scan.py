@@ -210,6 +210,30 @@ def disassemble_so(path):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def kernel_static_lds(path):
+    """{kernel symbol: .group_segment_fixed_size} from the gfx950 code objects' metadata notes
+    (static LDS: a kernel's dynamic LDS starts right after it)."""
+    tmp = tempfile.mkdtemp(prefix="dslds_")
+    try:
+        lib = os.path.join(tmp, "lib.so")
+        shutil.copy(path, lib)
+        subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", lib], cwd=tmp, check=True,
+                       capture_output=True)
+        out = {}
+        for f in sorted(os.listdir(tmp)):
+            if "amdgcn" in f and "gfx950" in f:
+                notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", os.path.join(tmp, f)],
+                                       check=True, capture_output=True, text=True).stdout
+                for block in notes.split("\n  - ")[1:]:
+                    name = re.search(r"^\s*\.name:\s+(\S+)", block, re.M)
+                    size = re.search(r"^\s*\.group_segment_fixed_size:\s+(\d+)", block, re.M)
+                    if name and size:
+                        out[name.group(1)] = int(size.group(1))
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def texts_of(path):
     if path.endswith(".s"):
         return [(os.path.basename(path), open(path).read())]

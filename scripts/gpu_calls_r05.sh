@@ -349,4 +349,19 @@ c20() {
   exit 0
 }
 
+c21() {
+  # window reads at raw LDS addresses (no add of the LDS symbol): trunk tests, then timed
+  # against the previous build (expbuild/prev) alternately
+  export OUT=gpurun_out/r05u
+  mkdir -p $OUT
+  run tests 400 python -u -m pytest tests/test_nn_gpu.py tests/test_net_golden_gpu.py -m gpu -x -v \
+    -p no:cacheprovider --timeout 120 --timeout-method thread \
+    -k "persistent or trunk_heads or golden or matches or two_board" || exit $?
+  for i in 1 2 3; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    run net_prev 120 env AZ_LIB_PATH=expbuild/prev/libaz_othello.so python scripts/net_time.py 1024 40
+  done
+  exit 0
+}
+
 "$@"

@@ -60,3 +60,15 @@ def test_library_has_no_packed_f32_result_stored_by_a_wide_lds_store():
     for name, text in texts:
         found += scan.scan_pk_stores(text, name)
     assert not found, "\n".join(f"{fn}: {prod} -> {st}" for _, fn, _, prod, st in found[:10])
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)),
+                    reason="needs the built library and llvm-objdump")
+def test_resident_trunk_kernels_have_no_static_lds():
+    """The resident trunk's window reads use raw LDS addresses (read_rows_x in
+    csrc/conv_wino4.hip): correct only while k_trunk_wino4's dynamic LDS starts at address 0,
+    i.e. the kernel declares no static LDS."""
+    sizes = scan.kernel_static_lds(LIB)
+    trunk = {k: v for k, v in sizes.items() if "k_trunk_wino4" in k}
+    assert trunk, "no k_trunk_wino4 kernel in the library's metadata"
+    assert all(v == 0 for v in trunk.values()), trunk
