@@ -254,8 +254,9 @@ c14() {
 
 c15() {
   # the final tree (resident trunk + residual staging): the whole GPU suite, smoke(), the bench
-  # line, a graph-mode kernel trace, the trunk's SQ / TA / L2 counters
-  export OUT=gpurun_out/r05o
+  # line, a graph-mode kernel trace, the trunk's SQ / TA / L2 counters (OUT overridable: r05o
+  # was the first final tree, r05v the one after the raw LDS addresses)
+  export OUT=${OUT:-gpurun_out/r05o}
   mkdir -p $OUT
   run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
     --timeout-method thread || exit $?
