@@ -458,7 +458,8 @@ def trunk_roofline(sp, device, n_boards):
                 + 2 * 128 * 65 + 2 * 64 * 256 + 2 * 256)
     algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
     return {"kernel": "k_trunk_wino4 (az_trunk_wino4_heads_gpu: stem + %d block convs, Winograd "
-                      "F(2x2,3x3) fp16x2, two boards per workgroup, + heads)" % n_convs,
+                      "F(2x2,3x3) fp16x2, two boards per workgroup, each layer's input resident "
+                      "in LDS, + heads)" % n_convs,
             "bound": "mfma", "achieved": round(algorithmic, 1), "peak": MFMA16_PEAK,
             "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": None,
             "achieved_basis": "algorithmic: the net's %.1f MFLOP per evaluation x boards / launch "
