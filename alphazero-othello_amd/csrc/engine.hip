@@ -54,6 +54,14 @@ constexpr int kMaxLeaves = 8;    // leaves_per_step limit (virtual-loss descents
 #ifndef AZ_SEL_LEVELS
 #define AZ_SEL_LEVELS 14
 #endif
+// K = 1 select: a terminal descent backs up from the path's N / W held in registers (lane d =
+// depth d, loaded by the descent itself) and patches the root's record and its children's
+// PUCT inputs in registers instead of reloading them -- two dependent round trips fewer per
+// terminal descent, the same stores and the same double additions; 0 = load N / W and reload
+// the root (A/B builds)
+#ifndef AZ_SEL_REGBACKUP
+#define AZ_SEL_REGBACKUP 0
+#endif
 #ifndef AZ_MOVE_KC
 #define AZ_MOVE_KC 4
 #endif
@@ -450,6 +458,7 @@ struct NodeRec {
   int visits;        // N
   int meta;          // flags | nchild << 8 | (uint8)tval << 16
   uint64_t own, opp; // the position (the leaf's NN input, without another load)
+  double wv;         // W (AZ_SEL_REGBACKUP: the terminal backup from registers)
 };
 
 __device__ __forceinline__ NodeRec load_rec(const Params& p, int g, int half, int node) {
@@ -461,6 +470,7 @@ __device__ __forceinline__ NodeRec load_rec(const Params& p, int g, int half, in
   r.meta = (int)p.a.flags[k] | ((int)p.a.nchild[k] << 8) | ((int)(uint8_t)p.a.tval[k] << 16);
   r.own = p.a.own[k];
   r.opp = p.a.opp[k];
+  r.wv = AZ_SEL_REGBACKUP ? p.a.W[k] : 0.0;
   return r;
 }
 __device__ __forceinline__ uint8_t rec_flags(const NodeRec& r) { return (uint8_t)r.meta; }
@@ -528,6 +538,7 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
     mine.visits = n;
     mine.own = k.own;
     mine.opp = k.opp;
+    mine.wv = w;
     const double q = -(n == 0 ? 0.0 : w / (double)n);
     if (f64) {
       const double u = p.c_puct * pr * sq / (double)(1 + n);
@@ -545,6 +556,7 @@ __device__ NodeRec select_child_rec(const Params& p, int g, int half, const Node
   r.meta = readlane(mine.meta, idx);
   r.own = readlane(mine.own, idx);
   r.opp = readlane(mine.opp, idx);
+  r.wv = AZ_SEL_REGBACKUP ? readlane(mine.wv, idx) : 0.0;
   return r;
 }
 
@@ -782,17 +794,53 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p,
     // keep returning a leaf or the finished search, as its fixed-length graph relies on
     int levels = 0;
     const bool level_budget = KMAX == 1 && AZ_SEL_LEVELS > 0 && p.auto_play;
+    constexpr bool RB = KMAX == 1 && AZ_SEL_REGBACKUP;
+    bool patched = false;  // RB: the root record and kid0 are current in registers
+    NodeRec root = cur;
+    int path_n = 0;        // RB: lane d: N and W of the node at depth d
+    double path_w = 0.0;
     while (sims_done + w.n < target && w.n < K && guard < max_descents &&
            (!level_budget || levels < AZ_SEL_LEVELS)) {
-      if (guard > 0) cur = load_root(p, g, half, kid0);  // the last backup changed the root's N
+      if (guard > 0) {  // the last backup changed the root's N
+        if (RB && patched)
+          cur = root;
+        else
+          cur = load_root(p, g, half, kid0);
+      }
+      root = cur;
+      patched = false;
       ++guard;
       depth = 0;
       path_node = 0;
+      if constexpr (RB) {
+        if (lane == 0) {
+          path_n = cur.visits;
+          path_w = cur.wv;
+        }
+      }
       while (true) {
         const uint8_t f = rec_flags(cur);
         if (f & kTerminal) {  // MCTS_model.py:381-384
           const double tv = (double)rec_tval(cur);
-          if (depth < kMaxPath) {
+          if (RB && depth < kMaxPath) {
+            // backup_path's stores from the N / W this descent loaded, then the root's record
+            // and its children's inputs patched the same way
+            if (lane <= depth) {
+              const int64_t k = nidx(p, half, g, path_node);
+              p.a.N[k] = path_n + 1;
+              p.a.W[k] = path_w + (((depth - lane) & 1) ? -tv : tv);
+            }
+            root.visits += 1;
+            root.wv = root.wv + ((depth & 1) ? -tv : tv);
+            if (depth >= 1) {
+              const int j1 = readlane(path_node, 1) - root.first;
+              if (lane == j1) {
+                kid0.n += 1;
+                kid0.w = kid0.w + (((depth - 1) & 1) ? -tv : tv);
+              }
+            }
+            patched = root.first == 1;  // kid0 holds the root's children only then
+          } else if (depth < kMaxPath) {
             backup_path(p, g, half, path_node, depth, tv);
           } else if (lane == 0) {
             backup(p, g, half, cur.node, tv);
@@ -813,6 +861,12 @@ __global__ __launch_bounds__(kSelBlock) void k_select(Params p,
         }
         ++depth;
         if (lane == depth) path_node = cur.node;
+        if constexpr (RB) {
+          if (lane == depth) {
+            path_n = cur.visits;
+            path_w = cur.wv;
+          }
+        }
       }
       levels += depth + 1;
     }

@@ -365,4 +365,20 @@ c21() {
   exit 0
 }
 
+c22() {
+  # the select launch's terminal backups from registers (AZ_SEL_REGBACKUP=1): the engine and
+  # bench-path parity tests on that build, then configs[2] benches alternated
+  export OUT=gpurun_out/r05w
+  mkdir -p $OUT
+  run rb_tests 900 env AZ_LIB_PATH=expbuild/rb/libaz_othello.so python -u -m pytest \
+    tests/test_bench_path_gpu.py tests/test_engine_gpu.py tests/test_vl_gpu.py \
+    tests/test_callers_gpu.py tests/test_fullwidth_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 300 --timeout-method thread || exit $?
+  for i in 1 2; do
+    run bench_tree 300 python bench.py --skip-cpu --skip-kernel
+    run bench_rb 300 env AZ_LIB_PATH=expbuild/rb/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+  done
+  exit 0
+}
+
 "$@"
