@@ -381,4 +381,20 @@ c22() {
   exit 0
 }
 
+c23() {
+  # HBM bytes of the bench's trunk launch (az_trunk_wino4_heads_gpu: stem + convs + heads),
+  # for roofline_trunk.traffic: FETCH_SIZE and WRITE_SIZE passes, and a kernel trace of it
+  export OUT=gpurun_out/r05x
+  mkdir -p $OUT
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    run hbm_$i 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/hbm_$i -o pmc -- \
+      python3 scripts/trunk_heads_one.py 1024 20 || exit $?
+  done
+  run trace 90 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+    python3 scripts/trunk_heads_one.py 1024 20
+  exit 0
+}
+
 "$@"
