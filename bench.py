@@ -457,11 +457,18 @@ def trunk_roofline(sp, device, n_boards):
     per_eval = (2 * 64 * C * 9 + 2 * 64 * C * C * 9 * n_convs + 2 * 64 * C * 3
                 + 2 * 128 * 65 + 2 * 64 * 256 + 2 * 256)
     algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
+    traffic = None  # HBM bytes per launch, PMC (scripts/gpu_calls_r05.sh c23), at B = 1,024
+    tj = os.path.join(ROOT, "profiles", "trunk_traffic.json")
+    if n_boards == 1024 and os.path.exists(tj):
+        try:
+            traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
     return {"kernel": "k_trunk_wino4 (az_trunk_wino4_heads_gpu: stem + %d block convs, Winograd "
                       "F(2x2,3x3) fp16x2, two boards per workgroup, each layer's input resident "
                       "in LDS, + heads)" % n_convs,
             "bound": "mfma", "achieved": round(algorithmic, 1), "peak": MFMA16_PEAK,
-            "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": traffic,
             "achieved_basis": "algorithmic: the net's %.1f MFLOP per evaluation x boards / launch "
                               "time" % (per_eval / 1e6),
             "mfma_executed_tflops": round(executed, 1),
