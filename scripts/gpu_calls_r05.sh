@@ -397,4 +397,16 @@ c23() {
   exit 0
 }
 
+c24() {
+  # configs[2] as two 512-slot pipelines on their own streams (one pipeline's select beside the
+  # other's trunk) against one pipeline, with the resident-input trunk; alternated
+  export OUT=gpurun_out/r05y
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_1p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel --pipelines 2
+  done
+  exit 0
+}
+
 "$@"
