@@ -409,4 +409,16 @@ c24() {
   exit 0
 }
 
+c25() {
+  # configs[2]'s leaf batch of 1,024 with two pipelines: 2,048 games as two 1,024-slot
+  # pipelines against one 1,024-slot pipeline, resident-input trunk; alternated
+  export OUT=gpurun_out/r05z
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_1p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_2x1024 300 python bench.py --skip-cpu --skip-kernel --games 2048 --pipelines 2
+  done
+  exit 0
+}
+
 "$@"
