@@ -421,4 +421,15 @@ c25() {
   exit 0
 }
 
+c26() {
+  # configs[3]'s 4,096 games per GPU as two 2,048-slot pipelines against one, resident trunk
+  export OUT=gpurun_out/r05aa
+  mkdir -p $OUT
+  for i in 1 2; do
+    run c4_1p 500 python bench.py --workload c4 --skip-cpu --skip-kernel --pipelines 1
+    run c4_2p 500 python bench.py --workload c4 --skip-cpu --skip-kernel --pipelines 2
+  done
+  exit 0
+}
+
 "$@"
