@@ -4,8 +4,10 @@
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU, RCCL)
 
 Workload (BASELINE.json configs[2], the one the metric is quoted on): 8x8 Othello,
-400 sims/move, AlphaZeroNet(8, 65, 5, 128) random init (no checkpoints offline), leaf batch
-1,024 = 1,024 concurrent games per GPU with one leaf each per step; the reference's
+400 sims/move, AlphaZeroNet(8, 65, 5, 128) random init (no checkpoints offline), batched leaf
+eval = 1,024: two pipelines of 1,024 concurrent games per GPU on their own HIP streams (one
+pipeline's select launch beside the other's trunk), each evaluating its games' one leaf per
+step as one batch of 1,024 (--pipelines 1: one 1,024-game pipeline); the reference's
 self-play settings (train.py:399-423): c_puct 2, Dirichlet alpha 1 / eps 0.3 at the root,
 temperature 1 for 35 plies then 0, lambda 0.98.  The net is fp32-accurate: the 3x3 trunk runs
 fp32 operands as exactly scaled fp16 hi + lo pairs, three fp16 MFMA products with fp32
@@ -14,8 +16,8 @@ kernel's, tests/test_nn_gpu.py); --conv-precision split3 / fp32 select the bf16x
 plain fp32 MFMA kernels.
 
 A step is one batched simulation over every game slot: select (descent + leaf pack) ->
-net forward -> expand+backup -> move phase; games restart as they finish (weak scaling:
-1,024 games per GPU).  Slot starts are staggered over one game length ((sims+1) x 60
+net forward -> expand+backup -> move phase (with two pipelines, one step of each); games
+restart as they finish (weak scaling: 2,048 games per GPU).  Slot starts are staggered over one game length ((sims+1) x 60
 steps) so that when the window opens every slot is playing and the slots' game phases are
 spread evenly over a game (the continuous self-play steady state: end-game simulations are
 cheaper, so a window at one game phase would mis-measure); the untimed warmup runs
@@ -123,8 +125,10 @@ def parse():
     ap.add_argument("--pipelines", type=int, default=None,
                     help="the GPU's games as this many independent pipelines, each on its own "
                          "HIP stream (engine.PipelinedSelfPlay: one pipeline's select launch "
-                         "overlaps another's trunk); default 2 for c2 and c5 (measured +8 / "
-                         "+10 %%), 1 for c3 and c4 (no gain / -4.5 %%: profiles/r04_pipelines_ab.json)")
+                         "overlaps another's trunk); default 2 for c2, c3 and c5 (measured +8 / "
+                         "+4.6 / +10 %%: profiles/r04_pipelines_ab.json, r05_pipelines_ab.json), 1 "
+                         "for c4; c3's default games = 1,024 per pipeline, so every evaluation "
+                         "is configs[2]'s batch of 1,024 leaves")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=None,
@@ -138,13 +142,16 @@ def parse():
               "arena": (1024, 400, "az5x128", False, "fp32"),
               "c4": (4096, 400, "az5x128", False, "fp32"),
               "c5": (4096, 400, "az5x128", True, "fp16")}[a.workload]
-    a.games = a.games or preset[0]
+    if a.pipelines is None:
+        a.pipelines = 2 if a.workload in ("c2", "c3", "c5") else 1
+    # c3 (configs[2]: "batched leaf eval = 1024"): 1,024 concurrent games per pipeline
+    a.games = a.games or (1024 * a.pipelines if a.workload == "c3" else preset[0])
     a.sims = a.sims or preset[1]
     a.net = a.net or preset[2]
     a.d4, a.precision = preset[3], preset[4]
     a.conv_precision = a.conv_precision or ("fp16" if a.precision == "fp16" else "fp16x2")
-    if a.pipelines is None:
-        a.pipelines = 2 if a.workload in ("c2", "c5") and a.games % 2 == 0 else 1
+    if a.games % a.pipelines:
+        a.pipelines = 1
     return a
 
 
@@ -849,7 +856,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": DTYPE_LABEL[a.conv_precision],
         "data": "synthetic: self-play from the initial position, random-init net weights",
         "config": {"workload": {"c3": "configs[2]: 8x8 Othello, 400 sims/move, AlphaZeroNet(5x128) "
-                                      "random init fp32, leaf batch 1024 = concurrent games",
+                                      "random init fp32, batched leaf eval = 1024 (each "
+                                      "pipeline's concurrent games, one leaf each per step)",
                                 "c2": "configs[1]: 8x8 Othello, 4096 concurrent games, 100 sims/move, "
                                       "FastOthelloNet random init fp32",
                                 "c4": "configs[3]: 8x8 Othello, 4096 concurrent games per GPU "
@@ -860,7 +868,8 @@ def main():
                                       "symmetry per leaf + fp16 net inference"}[a.workload],
                    "d4_augment": a.d4,
                    "games_per_gpu": a.games, "sims": a.sims, "net": a.net,
-                   "leaves_per_step": a.leaves, "leaf_batch": a.games * a.leaves,
+                   "leaves_per_step": a.leaves,
+                   "leaf_batch": a.games // a.pipelines * a.leaves,
                    "parallelism": f"dp{world} (independent games per GPU)",
                    "pipelines": a.pipelines,
                    "hip_graph": sp.graph is not None, "graph_error": sp.graph_error,
@@ -920,9 +929,10 @@ def main():
                                                            / 1e9 / HBM_PEAK_GBS, 4)}
     if rank == 0 and not a.skip_kernel and hasattr(sp.net, "c2") \
             and getattr(sp.net, "conv_impl", "") == "hip":
-        result["roofline_conv"] = conv_roofline(sp, device, a.games * a.leaves)
-        if a.games * a.leaves <= 4 * torch.cuda.get_device_properties(device).multi_processor_count:
-            rt = trunk_roofline(sp, device, a.games * a.leaves)
+        lb = a.games // a.pipelines * a.leaves  # one evaluation's boards
+        result["roofline_conv"] = conv_roofline(sp, device, lb)
+        if lb <= 4 * torch.cuda.get_device_properties(device).multi_processor_count:
+            rt = trunk_roofline(sp, device, lb)
             if rt is not None:
                 result["roofline_trunk"] = rt
     if rank == 0 and not a.skip_cpu:

@@ -1,6 +1,7 @@
 """Host side of the pipelined self-play (no GPU): the split is checked before anything is
-allocated, and bench.py pipelines configs[1] and configs[4] by default (measured gains), not
-configs[2] / configs[3]."""
+allocated, and bench.py pipelines configs[1], configs[2] and configs[4] by default (measured
+gains), not configs[3]; configs[2] keeps its batch of 1,024 leaves per evaluation (1,024 games per
+pipeline)."""
 import sys
 
 import pytest
@@ -17,10 +18,20 @@ def test_pipelines_must_divide_the_games():
         PipelinedSelfPlay(None, {"num_simulations": 8}, 64, pipelines=0)
 
 
-@pytest.mark.parametrize("argv,want", [([], 1), (["--workload", "c4"], 1),
+@pytest.mark.parametrize("argv,want", [([], 2), (["--workload", "c4"], 1),
                                        (["--workload", "c2"], 2), (["--workload", "c5"], 2),
                                        (["--pipelines", "2"], 2),
                                        (["--workload", "c5", "--games", "1023"], 1)])
 def test_bench_pipeline_defaults(monkeypatch, argv, want):
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
     assert bench.parse().pipelines == want
+
+
+@pytest.mark.parametrize("argv,games,pipes", [([], 2048, 2), (["--pipelines", "1"], 1024, 1),
+                                              (["--pipelines", "4"], 4096, 4),
+                                              (["--games", "1024"], 1024, 2)])
+def test_bench_configs2_leaf_batch(monkeypatch, argv, games, pipes):
+    """configs[2] ("batched leaf eval = 1024"): by default 1,024 games per pipeline."""
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    a = bench.parse()
+    assert (a.games, a.pipelines) == (games, pipes)
