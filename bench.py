@@ -125,10 +125,10 @@ def parse():
     ap.add_argument("--pipelines", type=int, default=None,
                     help="the GPU's games as this many independent pipelines, each on its own "
                          "HIP stream (engine.PipelinedSelfPlay: one pipeline's select launch "
-                         "overlaps another's trunk); default 2 for c2, c3 and c5 (measured +8 / "
-                         "+4.6 / +10 %%: profiles/r04_pipelines_ab.json, r05_pipelines_ab.json), 1 "
-                         "for c4; c3's default games = 1,024 per pipeline, so every evaluation "
-                         "is configs[2]'s batch of 1,024 leaves")
+                         "overlaps another's trunk); default 2 (measured c2 +8, c3 +4.6, c4 "
+                         "+2, c5 +10 %%: profiles/r04_pipelines_ab.json, r05_pipelines_ab.json); "
+                         "c3's default games = 1,024 per pipeline, so every evaluation is "
+                         "configs[2]'s batch of 1,024 leaves")
     ap.add_argument("--kernel-n", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=None,
@@ -143,7 +143,7 @@ def parse():
               "c4": (4096, 400, "az5x128", False, "fp32"),
               "c5": (4096, 400, "az5x128", True, "fp16")}[a.workload]
     if a.pipelines is None:
-        a.pipelines = 2 if a.workload in ("c2", "c3", "c5") else 1
+        a.pipelines = 2 if a.workload in ("c2", "c3", "c4", "c5") else 1
     # c3 (configs[2]: "batched leaf eval = 1024"): 1,024 concurrent games per pipeline
     a.games = a.games or (1024 * a.pipelines if a.workload == "c3" else preset[0])
     a.sims = a.sims or preset[1]

@@ -1,7 +1,6 @@
 """Host side of the pipelined self-play (no GPU): the split is checked before anything is
-allocated, and bench.py pipelines configs[1], configs[2] and configs[4] by default (measured
-gains), not configs[3]; configs[2] keeps its batch of 1,024 leaves per evaluation (1,024 games per
-pipeline)."""
+allocated, and bench.py pipelines every workload by default (measured gains); configs[2] keeps
+its batch of 1,024 leaves per evaluation (1,024 games per pipeline)."""
 import sys
 
 import pytest
@@ -18,7 +17,7 @@ def test_pipelines_must_divide_the_games():
         PipelinedSelfPlay(None, {"num_simulations": 8}, 64, pipelines=0)
 
 
-@pytest.mark.parametrize("argv,want", [([], 2), (["--workload", "c4"], 1),
+@pytest.mark.parametrize("argv,want", [([], 2), (["--workload", "c4"], 2),
                                        (["--workload", "c2"], 2), (["--workload", "c5"], 2),
                                        (["--pipelines", "2"], 2),
                                        (["--workload", "c5", "--games", "1023"], 1)])
