@@ -432,4 +432,16 @@ c26() {
   exit 0
 }
 
+c27() {
+  # configs[2] with three / four 1,024-game pipelines against the two-pipeline default
+  export OUT=gpurun_out/r05ac
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_3p 400 python bench.py --skip-cpu --skip-kernel --pipelines 3
+    run bench_4p 400 python bench.py --skip-cpu --skip-kernel --pipelines 4
+  done
+  exit 0
+}
+
 "$@"
