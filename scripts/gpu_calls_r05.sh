@@ -444,4 +444,15 @@ c27() {
   exit 0
 }
 
+c28() {
+  # one vs two 1,024-game pipelines again, alternated three times on one box
+  export OUT=gpurun_out/r05ad
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run bench_1p 300 python bench.py --skip-cpu --skip-kernel --pipelines 1
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+  done
+  exit 0
+}
+
 "$@"
