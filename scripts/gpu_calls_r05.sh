@@ -455,4 +455,18 @@ c28() {
   exit 0
 }
 
+c29() {
+  # round-3 scheduling knobs re-tested on the resident trunk: sched_group_barrier interleave
+  # (AZ_W4_SCHED 1 / 2 VALU per MFMA), s_setprio around the MFMA clusters (AZ_W4_PRIO=2)
+  export OUT=gpurun_out/r05ae
+  mkdir -p $OUT
+  for i in 1 2; do
+    run net_tree 120 python scripts/net_time.py 1024 40
+    for v in s1 s2 p2; do
+      run net_$v 120 env AZ_LIB_PATH=expbuild/$v/libaz_othello.so python scripts/net_time.py 1024 40
+    done
+  done
+  exit 0
+}
+
 "$@"
