@@ -469,4 +469,18 @@ c29() {
   exit 0
 }
 
+c30() {
+  # the merged select + move launch reserves the move phase's 64 KiB of LDS for every select
+  # workgroup: beside the other pipeline's trunk it blocks the trunk's second workgroup on
+  # a CU.  Moves in their own launch (--no-defer) against the default, two and one pipelines
+  export OUT=gpurun_out/r05af
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_2p_nodefer 300 python bench.py --skip-cpu --skip-kernel --no-defer
+    run bench_1p_nodefer 300 python bench.py --skip-cpu --skip-kernel --no-defer --pipelines 1
+  done
+  exit 0
+}
+
 "$@"
