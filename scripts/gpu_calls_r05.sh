@@ -483,4 +483,21 @@ c30() {
   exit 0
 }
 
+c31() {
+  # the deferred move phase as a forked launch (AZ_SEL_FORK=1: the select launch reserves no
+  # LDS): the engine / bench-path / pipelined parity tests with it, then benches
+  export OUT=gpurun_out/r05ag
+  mkdir -p $OUT
+  run fork_tests 900 env AZ_SEL_FORK=1 python -u -m pytest tests/test_bench_path_gpu.py \
+    tests/test_engine_gpu.py tests/test_pipelined_gpu.py tests/test_vl_gpu.py -m gpu -x -v \
+    -p no:cacheprovider --timeout 300 --timeout-method thread || exit $?
+  for i in 1 2; do
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_2p_fork 300 env AZ_SEL_FORK=1 python bench.py --skip-cpu --skip-kernel
+    run bench_1p 300 python bench.py --skip-cpu --skip-kernel --pipelines 1
+    run bench_1p_fork 300 env AZ_SEL_FORK=1 python bench.py --skip-cpu --skip-kernel --pipelines 1
+  done
+  exit 0
+}
+
 "$@"
