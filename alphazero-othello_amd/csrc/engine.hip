@@ -2049,11 +2049,6 @@ struct az_engine {
   uint64_t* d_opp = nullptr;
   float* d_zero_eval = nullptr;  // rollout mode: zeroed [G*K, 66] stand-in priors / values
   size_t lds_move = 0;
-  // AZ_SEL_FORK: the deferred move phase as its own launch on a forked stream beside the
-  // select launch (joined before the caller's next work), so the select workgroups reserve no
-  // LDS -- in the merged launch every workgroup reserves the move phase's re-root scratch
-  hipStream_t s_move = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -2079,11 +2074,6 @@ int dalloc(az_engine* e, T** ptr, size_t count) {
 void free_all(az_engine* e) {
   for (void* q : e->allocs) (void)hipFree(q);
   e->allocs.clear();
-  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-  if (e->s_move) (void)hipStreamDestroy(e->s_move);
-  e->ev_fork = e->ev_join = nullptr;
-  e->s_move = nullptr;
 }
 
 unsigned sel_grid(const az_engine* e) {
@@ -2229,16 +2219,6 @@ int az_engine_create(const az_config* cfg_in, az_engine** out) {
     return rc;
   }
   e->lds_move = (size_t)p.C * sizeof(int32_t);
-  if (const char* fk = getenv("AZ_SEL_FORK"); fk && atoi(fk) != 0) {
-    // the forked move launch's stream and events (created here: never during a capture)
-    if (hipStreamCreateWithFlags(&e->s_move, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
-      free_all(e);
-      delete e;
-      return azc::set_error(AZ_ERR_HIP, "AZ_SEL_FORK: stream / event creation failed");
-    }
-  }
   if (hipFuncSetAttribute((const void*)k_move, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)e->lds_move) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_reroot, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2446,38 +2426,8 @@ int az_select_move_expand(az_engine* e, float* nn_in, int32_t* leaf_o, const flo
     priors = e->d_zero_eval;
     values = e->d_zero_eval + (size_t)e->p.G * e->p.K * 65;
   }
-  hipStream_t s = azc::as_stream(stream);
-  static const bool fork = [] {
-    const char* v = getenv("AZ_SEL_FORK");
-    return v && atoi(v) != 0;
-  }();
-  if (fork) {
-    AZ_REQUIRE(e->s_move, AZ_ERR_STATE, "AZ_SEL_FORK set after the engine was created");
-    // fork: the move-only launch (the merged kernel's first move_blocks workgroups, same
-    // parity argument) on s_move, the select launch without them (no dynamic LDS) on s; join
-    const int mb = move_blocks_for(e);
-    AZ_HIP(hipEventRecord(e->ev_fork, s));
-    AZ_HIP(hipStreamWaitEvent(e->s_move, e->ev_fork, 0));
-    const dim3 grid((unsigned)mb);
-    if (e->p.K == 1)
-      hipLaunchKernelGGL((k_select<1, true>), grid, dim3(kSelBlock), e->lds_move, e->s_move,
-                         e->p, nullptr, nullptr, 0, par, mb, nullptr, nullptr);
-    else if (e->p.K <= 2)
-      hipLaunchKernelGGL((k_select<2, true>), grid, dim3(kSelBlock), e->lds_move, e->s_move,
-                         e->p, nullptr, nullptr, 0, par, mb, nullptr, nullptr);
-    else if (e->p.K <= 4)
-      hipLaunchKernelGGL((k_select<4, true>), grid, dim3(kSelBlock), e->lds_move, e->s_move,
-                         e->p, nullptr, nullptr, 0, par, mb, nullptr, nullptr);
-    else
-      hipLaunchKernelGGL((k_select<kMaxLeaves, true>), grid, dim3(kSelBlock), e->lds_move,
-                         e->s_move, e->p, nullptr, nullptr, 0, par, mb, nullptr, nullptr);
-    AZ_HIP(hipGetLastError());
-    const int rc = launch_select(e, nn_in, leaf_o, par, 0, s, priors, values, true);
-    AZ_HIP(hipEventRecord(e->ev_join, e->s_move));
-    AZ_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
-    return rc;
-  }
-  return launch_select(e, nn_in, leaf_o, par, move_blocks_for(e), s, priors, values, true);
+  return launch_select(e, nn_in, leaf_o, par, move_blocks_for(e), azc::as_stream(stream),
+                       priors, values, true);
 }
 
 int az_select_expand(az_engine* e, float* nn_in, int32_t* leaf_o, const float* priors,
