@@ -500,4 +500,18 @@ c31() {
   exit 0
 }
 
+c32() {
+  # host-side knobs with two pipelines: steps per HIP graph (8 default), the select launch's
+  # descent cap (AZ_MAX_DESCENTS, 4 default)
+  export OUT=gpurun_out/r05ah
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_def 300 python bench.py --skip-cpu --skip-kernel
+    run bench_spg16 300 python bench.py --skip-cpu --skip-kernel --steps-per-graph 16
+    run bench_md8 300 env AZ_MAX_DESCENTS=8 python bench.py --skip-cpu --skip-kernel
+    run bench_md2 300 env AZ_MAX_DESCENTS=2 python bench.py --skip-cpu --skip-kernel
+  done
+  exit 0
+}
+
 "$@"
