@@ -514,4 +514,15 @@ c32() {
   exit 0
 }
 
+c33() {
+  # the four-board resident trunk (one workgroup per CU, all 160 KiB) with two pipelines
+  export OUT=gpurun_out/r05ai
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_2p_tb4 300 env AZ_LIB_PATH=expbuild/tb4/libaz_othello.so python bench.py --skip-cpu --skip-kernel
+  done
+  exit 0
+}
+
 "$@"
