@@ -525,4 +525,13 @@ c33() {
   exit 0
 }
 
+c34() {
+  # the pipelined test with bench.py's configs[2] shape (2 x 1,024 games)
+  export OUT=gpurun_out/r05aj
+  mkdir -p $OUT
+  run pytest_pipe 400 python -u -m pytest tests/test_pipelined_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 300 --timeout-method thread || exit $?
+  exit 0
+}
+
 "$@"

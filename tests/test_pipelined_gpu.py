@@ -36,10 +36,13 @@ def _net(kind):
     return AlphaZeroNet(8, 65, 5, 128), {}  # fp16x2 persistent trunk + heads-fused conv
 
 
-@pytest.mark.parametrize("use_graph,kind", [(True, "mock"), (False, "mock"), (True, "az5x128"),
-                                            (True, "fast"), (True, "c5")])
-def test_pipelines_play_the_standalone_games(use_graph, kind):
-    G, P, steps = 512, 2, 1300
+# G = 2,048: bench.py's configs[2] default shape (two 1,024-game pipelines, each evaluation a
+# batch of 1,024 leaves on the persistent trunk, the two trunks on two streams)
+@pytest.mark.parametrize("use_graph,kind,G", [(True, "mock", 512), (False, "mock", 512),
+                                              (True, "az5x128", 512), (True, "fast", 512),
+                                              (True, "c5", 512), (True, "az5x128", 2048)])
+def test_pipelines_play_the_standalone_games(use_graph, kind, G):
+    P, steps = 2, 1300
     net, extra = _net(kind)
     kw = dict(seed=5, use_graph=use_graph, sample_capacity=G * 400, **extra)
     pp = PipelinedSelfPlay(net, ARGS, G, pipelines=P, **kw)
