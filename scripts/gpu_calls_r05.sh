@@ -534,4 +534,17 @@ c34() {
   exit 0
 }
 
+c35() {
+  # configs[4] (fp16 + D4): the direct fp16 conv (default) against the per-layer fp16 Winograd
+  # conv (AZ_CONV_ALGO=wino4), speed and the fp16 accuracy tests
+  export OUT=gpurun_out/r05ak
+  mkdir -p $OUT
+  run bench_c5 300 python bench.py --workload c5 --skip-cpu --skip-kernel
+  run bench_c5_w4 300 env AZ_CONV_ALGO=wino4 python bench.py --workload c5 --skip-cpu --skip-kernel
+  run bench_c5_w 300 env AZ_CONV_ALGO=wino python bench.py --workload c5 --skip-cpu --skip-kernel
+  run pytest_w4 400 env AZ_CONV_ALGO=wino4 python -u -m pytest tests/test_c5_gpu.py tests/test_net_golden_gpu.py \
+    -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread
+  exit 0
+}
+
 "$@"
