@@ -532,7 +532,12 @@ class PipelinedSelfPlay:
                       for i in range(pipelines)]
         p0 = self.parts[0]
         self.device = p0.device
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.parts]
+        # AZ_PIPE_PRIO (experiments): comma-separated stream priorities per pipeline (lower =
+        # higher priority; torch.cuda.Stream.priority_range())
+        pr = [int(x) for x in os.environ.get("AZ_PIPE_PRIO", "").split(",") if x.strip()]
+        self.streams = [torch.cuda.Stream(device=self.device,
+                                          priority=pr[i] if i < len(pr) else 0)
+                        for i in range(len(self.parts))]
         self.args, self.net = p0.args, p0.net
         self.defer_moves, self.engine_stem = p0.defer_moves, p0.engine_stem
 

@@ -547,4 +547,16 @@ c35() {
   exit 0
 }
 
+c36() {
+  # stream priorities of the two pipelines (AZ_PIPE_PRIO)
+  export OUT=gpurun_out/r05am
+  mkdir -p $OUT
+  run prio_range 60 python -c "import torch; print(torch.cuda.Stream.priority_range())"
+  for i in 1 2; do
+    run bench_2p 300 python bench.py --skip-cpu --skip-kernel
+    run bench_prio_hi_lo 300 env AZ_PIPE_PRIO=-1,0 python bench.py --skip-cpu --skip-kernel
+  done
+  exit 0
+}
+
 "$@"
