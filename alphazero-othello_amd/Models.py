@@ -633,6 +633,18 @@ class FusedInferenceNet(nn.Module, Inference):
                     return None
                 h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0], **sk)
             return h
+        elif heads_into is not None and not stem_done and self._trunk4_fp16_ready(c1s, c2s):
+            # fp16 wino4 convs: the stem, the tower and the heads in one persistent launch
+            # per chunk of resident boards (az_trunk_wino4_heads_fp16_gpu)
+            B = x.shape[0]
+            bufs = self._scratch(x.device, B)["absmax"]
+            cap = self._trunk4_cap(c1s[0].wq.device)
+            for b0 in range(0, B, cap):
+                b1 = min(B, b0 + cap)
+                self._trunk4_heads(None, [bufs[0][b0:b1], bufs[1][b0:b1]], c1s,
+                                   (heads_into[0][b0:b1], heads_into[1][b0:b1]),
+                                   planes=x[b0:b1], fp16=True)
+            return None
         else:
             h = self.stem(x)
         for c1, c2 in zip(c1s, c2s):
@@ -680,6 +692,29 @@ class FusedInferenceNet(nn.Module, Inference):
                                      device=dev)}
         return True
 
+    # AZ_TRUNK_FP16 (default on): fp16 wino4 convs (AZ_CONV_ALGO=wino4 at fp16) run as the
+    # persistent trunk with the stem and heads (az_trunk_wino4_heads_fp16_gpu) when the caller
+    # takes priors / values; 0 = per-layer launches
+    trunk_fp16 = os.environ.get("AZ_TRUNK_FP16", "1") == "1"
+
+    def _trunk4_fp16_ready(self, c1s, c2s):
+        convs = c1s + c2s
+        if not (self.trunk_fp16 and self.fuse_trunk4 and self.trunk_heads and convs
+                and isinstance(self.stem, _HipStem) and self._fused_heads_ready()
+                and os.environ.get("AZ_W4_BOARDS", "2") == "2"):
+            return False
+        if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16"
+                   and c.channels == 128 for c in convs):
+            return False
+        if not hasattr(self, "_t4"):
+            dev = convs[0].wq.device
+            order = [c for pair in zip(c1s, c2s) for c in pair]  # layer order
+            self._t4 = {
+                "wq": torch.tensor([c.wq.data_ptr() for c in order], dtype=torch.int64, device=dev),
+                "bias": torch.tensor([c.bias.data_ptr() for c in order], dtype=torch.int64,
+                                     device=dev)}
+        return True
+
     def _trunk4(self, h, bufs, c1s, c2s, heads_into, planes=None):
         """The tower on az_trunk_wino4_gpu: all 2n convs (returns the output), or with
         heads_into the first 2n - 1 and the last conv with the heads fused (returns None).
@@ -720,8 +755,9 @@ class FusedInferenceNet(nn.Module, Inference):
     # the separate heads-fused conv launch
     trunk_heads = os.environ.get("AZ_TRUNK_HEADS", "1") == "1"
 
-    def _trunk4_heads(self, h, bufs, c1s, heads_into, planes=None):
-        """The whole tower and the heads in one az_trunk_wino4_heads_gpu launch."""
+    def _trunk4_heads(self, h, bufs, c1s, heads_into, planes=None, fp16=False):
+        """The whole tower and the heads in one az_trunk_wino4_heads_gpu launch (fp16: the
+        fp16 wino4 convs', az_trunk_wino4_heads_fp16_gpu)."""
         import az_native as nat
 
         C = c1s[0].channels
@@ -736,14 +772,15 @@ class FusedInferenceNet(nn.Module, Inference):
         st = self.stem if planes is not None else None
         hw = self._hw
         priors, values = heads_into
-        nat.check(nat.lib.az_trunk_wino4_heads_gpu(
+        fn = "az_trunk_wino4_heads_fp16_gpu" if fp16 else "az_trunk_wino4_heads_gpu"
+        nat.check(getattr(nat.lib, fn)(
             nat.ptr(self._t4["wq"]), nat.ptr(self._t4["bias"]), nat.ptr(planes),
             nat.ptr(st.w9) if st is not None else None, nat.ptr(st.bias) if st is not None else None,
             nat.ptr(h), nat.ptr(hb[0]), nat.ptr(hb[1]), nat.ptr(t), nat.ptr(bufs[0]),
             nat.ptr(bufs[1]), B, 2 * len(c1s), C, nat.ptr(hw["wpv"]), nat.ptr(hw["bpv"]),
             nat.ptr(hw["wpolT"]), nat.ptr(hw["bpol"]), nat.ptr(hw["w1T"]), nat.ptr(hw["b1"]),
             nat.ptr(hw["w2"]), nat.ptr(hw["b2"]), nat.ptr(priors), nat.ptr(values),
-            nat.stream_ptr()), "az_trunk_wino4_heads_gpu")
+            nat.stream_ptr()), fn)
         return None
 
     def _fused_heads_ready(self):

@@ -252,8 +252,11 @@ struct W4 {
   // input X = [board][64 positions][C] fp32 (channel chunk slots swizzled by column pair,
   // xoff), V buffer 1 -- so a board-edge window's out-of-board rows and columns land in
   // finite words (X, or V's fp16 pairs, never an fp32 Inf / NaN pattern) and are masked
-  static constexpr int XOFF = BUF, XBYTES = BOARDS * 64 * C * 4, V1R = BUF + XBYTES;
-  static constexpr int RSD_BYTES = 2 * BUF + XBYTES;
+  // VPAD: V buffer 0 / 1 rounded up to the 8 KiB a board-edge window reaches before / past X
+  // (one board row plus one position: 4.5 KiB); FP16X2's buffers are that size, FP16's half
+  static constexpr int VPAD = BUF < 8192 ? 8192 : BUF;
+  static constexpr int XOFF = VPAD, XBYTES = BOARDS * 64 * C * 4, V1R = VPAD + XBYTES;
+  static constexpr int RSD_BYTES = 2 * VPAD + XBYTES;
   static constexpr int TRUNK_LDS =
       AZ_W4_RESIDENT && RSD_BYTES > LDS_BYTES ? RSD_BYTES : LDS_BYTES;
   static constexpr int LD_PER_THREAD = BOARDS * 64 * 4 / THREADS;  // 16-byte loads per chunk
@@ -1056,7 +1059,9 @@ __device__ __forceinline__ void heads_epilogue(St<G>& S, const HeadsOut& ho, int
   constexpr int C = G::C, NB = G::BOARDS;
   constexpr int IMG = NB * 64 * C * 4;  // the image; p [NB][128] and v [NB][64] after it
   static_assert(NB <= azh::kQuarters && G::THREADS >= 64 * azh::kQuarters, "heads layout");
-  static_assert(IMG + NB * (128 + 64) * 4 <= G::LDS_BYTES, "heads LDS");
+  // (the FP16 heads conv runs only as the resident trunk's last layer, in TRUNK_LDS)
+  static_assert(IMG + NB * (128 + 64) * 4 <= (G::SCALED ? G::LDS_BYTES : G::TRUNK_LDS),
+                "heads LDS");
   // the partial sums (lp at 0, hv at 4,352) overlay the image's first board, written after
   // heads_four's first barrier, when no wave reads the image any more
   static_assert(azh::kQuarters * NB * 65 * 4 <= 4352 &&
@@ -1119,9 +1124,9 @@ __device__ __forceinline__ void conv_body(
                 "the layer hand-off is the persistent two-board fp16x2 trunk's");
   static_assert(!(RSD || XFILL || XOUT) ||
                     (RSD && !HIN && !HOUT && (G::BOARDS == 2 || G::BOARDS == 4) && G::NRT == 1 &&
-                     G::SCALED &&
+                     (G::SCALED || G::MODE == AZ_CONV_FP16) &&
                      !G::SPLIT && LAUNDER && AZ_W4_DIET && C == 128),
-                "the resident input is the persistent two-board fp16x2 trunk's");
+                "the resident input is the persistent two-board fp16x2 / fp16 trunk's");
   constexpr bool NOY = RSD && XOUT && !RES && !HEADS;
 
   extern __shared__ float4 lds4[];
@@ -1235,7 +1240,7 @@ __device__ __forceinline__ void conv_body(
       // V buffers zeroed (a board-edge window reads some of their words: finite from here on),
       // and the whole input into X: 16 loads of 16 bytes per thread, in two halves
 #pragma unroll
-      for (int i = tid * 16; i < G::BUF; i += G::THREADS * 16) {
+      for (int i = tid * 16; i < G::VPAD; i += G::THREADS * 16) {
         *reinterpret_cast<f32x4*>(S.lds + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         *reinterpret_cast<f32x4*>(S.lds + G::V1R + i) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
@@ -1681,7 +1686,7 @@ __global__ __launch_bounds__(G::THREADS, 2 / G::NRT) void k_trunk_wino4(TrunkW4 
     }
     return;
   }
-  constexpr bool HO = AZ_W4_HANDOFF != 0 && G::BOARDS == 2;  // the hand-off: two-board only
+  constexpr bool HO = AZ_W4_HANDOFF != 0 && G::BOARDS == 2 && G::SCALED;  // two-board fp16x2 only
   for (int i = 0; i < n_loop; ++i) {
     if (i > 0) layer_fence();
     // a conv whose output the next conv reads hands it off through LDS (every conv but the
@@ -1992,7 +1997,8 @@ extern "C" int az_trunk_wino4_gpu(const void* const* wq, const float* const* bia
   return AZ_OK;
 }
 
-extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* const* bias,
+template <int MODE>
+static int trunk_heads_entry(const char* fn, const void* const* wq, const float* const* bias,
                                         const float* planes, const float* stem_w,
                                         const float* stem_b, float* h_in, float* hb0,
                                         float* hb1, float* t, float* amax0, float* amax1,
@@ -2004,25 +2010,25 @@ extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* cons
                                         void* stream) {
   AZ_REQUIRE(n_boards >= 0 && n_boards <= kW4MaxBoards && n_convs >= 2 && n_convs % 2 == 0,
              AZ_ERR_ARG,
-             "az_trunk_wino4_heads_gpu: n_boards %d (<= %d) / n_convs %d (even, >= 2)", n_boards,
+             "%s: n_boards %d (<= %d) / n_convs %d (even, >= 2)", fn, n_boards,
              kW4MaxBoards, n_convs);
   if (n_boards == 0) return AZ_OK;
   AZ_REQUIRE(wq && bias && h_in && hb0 && hb1 && t && amax0 && amax1, AZ_ERR_ARG,
-             "az_trunk_wino4_heads_gpu: null buffer");
+             "%s: null buffer", fn);
   AZ_REQUIRE(h_in != hb0 && h_in != hb1 && h_in != t && hb0 != hb1 && hb0 != t && hb1 != t &&
                  amax0 != amax1,
-             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: aliased buffers");
+             AZ_ERR_ARG, "%s: aliased buffers", fn);
   AZ_REQUIRE(((uintptr_t)h_in | (uintptr_t)hb0 | (uintptr_t)hb1 | (uintptr_t)t) % 16 == 0,
-             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: buffers must be 16-byte aligned");
+             AZ_ERR_ARG, "%s: buffers must be 16-byte aligned", fn);
   AZ_REQUIRE(channels == 128, AZ_ERR_ARG,
-             "az_trunk_wino4_heads_gpu: channels must be 128, got %d", channels);
+             "%s: channels must be 128, got %d", fn, channels);
   AZ_REQUIRE(!planes || (stem_w && stem_b && ((uintptr_t)stem_w | (uintptr_t)stem_b) % 16 == 0),
-             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: planes without 16-byte aligned stem weights");
+             AZ_ERR_ARG, "%s: planes without 16-byte aligned stem weights", fn);
   AZ_REQUIRE(wpv && bpv && wpolT && bpol && w1T && b1 && w2 && b2 && priors && values,
-             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: null heads buffer");
+             AZ_ERR_ARG, "%s: null heads buffer", fn);
   AZ_REQUIRE(((uintptr_t)wpv | (uintptr_t)w1T | (uintptr_t)b1 | (uintptr_t)w2) % 16 == 0,
-             AZ_ERR_ARG, "az_trunk_wino4_heads_gpu: heads weights must be 16-byte aligned");
-  using G = W4<AZ_CONV_FP16X2, 1, AZ_W4_TRUNK_BOARDS>;  // two-board workgroups, FP16X2
+             AZ_ERR_ARG, "%s: heads weights must be 16-byte aligned", fn);
+  using G = W4<MODE, 1, AZ_W4_TRUNK_BOARDS>;  // two-board workgroups
   static bool attr_set = false;
   if (!attr_set) {
     AZ_HIP(hipFuncSetAttribute((const void*)k_trunk_wino4<G, true>,
@@ -2038,6 +2044,28 @@ extern "C" int az_trunk_wino4_heads_gpu(const void* const* wq, const float* cons
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
+
+
+#define AZ_TRUNK_HEADS_ARGS                                                                     \
+  const void *const *wq, const float *const *bias, const float *planes, const float *stem_w,   \
+      const float *stem_b, float *h_in, float *hb0, float *hb1, float *t, float *amax0,        \
+      float *amax1, int32_t n_boards, int32_t n_convs, int32_t channels, const float *wpv,     \
+      const float *bpv, const float *wpolT, const float *bpol, const float *w1T,                \
+      const float *b1, const float *w2, const float *b2, float *priors, float *values,          \
+      void *stream
+#define AZ_TRUNK_HEADS_PASS                                                                     \
+  wq, bias, planes, stem_w, stem_b, h_in, hb0, hb1, t, amax0, amax1, n_boards, n_convs,         \
+      channels, wpv, bpv, wpolT, bpol, w1T, b1, w2, b2, priors, values, stream
+extern "C" int az_trunk_wino4_heads_gpu(AZ_TRUNK_HEADS_ARGS) {
+  return trunk_heads_entry<AZ_CONV_FP16X2>("az_trunk_wino4_heads_gpu", AZ_TRUNK_HEADS_PASS);
+}
+// the same launch in FP16 (one fp16 product per MFMA step, no operand scaling; the weights
+// prepared for the FP16 wino4 conv): configs[4]'s fp16 inference
+extern "C" int az_trunk_wino4_heads_fp16_gpu(AZ_TRUNK_HEADS_ARGS) {
+  return trunk_heads_entry<AZ_CONV_FP16>("az_trunk_wino4_heads_fp16_gpu", AZ_TRUNK_HEADS_PASS);
+}
+#undef AZ_TRUNK_HEADS_ARGS
+#undef AZ_TRUNK_HEADS_PASS
 
 extern "C" int az_conv3x3_wino4_gpu(const float* x, const void* wq, const float* bias,
                                     const float* res, float* y, int32_t n_boards,

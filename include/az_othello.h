@@ -482,6 +482,20 @@ int az_trunk_wino4_heads_gpu(const void* const* wq, const float* const* bias,
                              const float* w2, const float* b2, float* priors, float* values,
                              void* stream);
 
+/* az_trunk_wino4_heads_gpu in fp16 (configs[4]'s fp16 inference): one fp16 product per
+ * MFMA step, no operand scaling, the block convs' weights prepared for the fp16 wino4 conv
+ * (az_conv3x3_wino_prep_gpu with AZ_CONV_FP16); same buffers and heads.  Bit-identical to the
+ * per-layer fp16 wino4 convs + the separate heads kernel.  Replaces the same reference span
+ * (Models.py:205-221) at configs[4]'s precision. */
+int az_trunk_wino4_heads_fp16_gpu(const void* const* wq, const float* const* bias,
+                                  const float* planes, const float* stem_w, const float* stem_b,
+                                  float* h_in, float* hb0, float* hb1, float* t, float* amax0,
+                                  float* amax1, int32_t n_boards, int32_t n_convs,
+                                  int32_t channels, const float* wpv, const float* bpv,
+                                  const float* wpolT, const float* bpol, const float* w1T,
+                                  const float* b1, const float* w2, const float* b2,
+                                  float* priors, float* values, void* stream);
+
 /* ---------------- replay buffer (device) -------------------------------------------
  * Trainer._aggregate_duplicates (reference train.py:142-173) on bitboard rows: rows with
  * equal (own, opp, version) — the reference's (sha1(canonical int8 board), version) —

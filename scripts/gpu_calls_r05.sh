@@ -559,4 +559,23 @@ c36() {
   exit 0
 }
 
+c37() {
+  # the fp16 persistent trunk (az_trunk_wino4_heads_fp16_gpu): parity, then configs[4] with the
+  # fp16 wino4 convs on it against the direct fp16 default
+  export OUT=gpurun_out/r05an
+  mkdir -p $OUT
+  run pytest_fp16trunk 300 python -u -m pytest tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 120 --timeout-method thread || exit $?
+  run pytest_c5_w4 400 env AZ_CONV_ALGO=wino4 python -u -m pytest tests/test_c5_gpu.py tests/test_pipelined_gpu.py \
+    -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread || exit $?
+  for i in 1 2; do
+    run bench_c5 300 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+    run bench_c5_w4t 300 env AZ_CONV_ALGO=wino4 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+  done
+  run net_fp16_direct 120 python scripts/net_time.py 1024 40 fp16
+  run net_fp16 120 env AZ_CONV_ALGO=wino4 python scripts/net_time.py 1024 40 fp16
+  run net_fp16_w4_layers 120 env AZ_CONV_ALGO=wino4 AZ_TRUNK_FP16=0 python scripts/net_time.py 1024 40 fp16
+  exit 0
+}
+
 "$@"

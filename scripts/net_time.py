@@ -2,7 +2,7 @@
 trunk + heads-fused last conv) at B boards, replayed from a HIP graph of 20 evaluations on
 random positions; the library is AZ_LIB_PATH's (experiment builds) or the tree's.  One JSON
 line: median / min microseconds per evaluation over `reps` replays.
-    python scripts/net_time.py [B] [reps]"""
+    python scripts/net_time.py [B] [reps] [fp16]   (fp16: configs[4]'s fp16 inference copy)"""
 import json
 import os
 import sys
@@ -17,7 +17,8 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 torch.manual_seed(0)
 net = AlphaZeroNet(8, 65, 5, 128).cuda().eval()
-m = inference_copy(net, "cuda")
+fp16 = len(sys.argv) > 3 and sys.argv[3] == "fp16"
+m = inference_copy(net, "cuda", dtype=torch.float16) if fp16 else inference_copy(net, "cuda")
 x = torch.randint(-1, 2, (B, 64), device="cuda").float()
 pr = torch.empty(B, 65, device="cuda")
 va = torch.empty(B, device="cuda")

@@ -104,3 +104,23 @@ def test_fused_batch1_inference_matches_reference(kind, fx):
         pi, v = fused.inference(s, int(p))
         np.testing.assert_allclose(pi, pol, atol=1e-5, rtol=1e-4)
         assert abs(v - val) <= 1e-5 + 1e-4 * abs(val)
+
+
+@pytest.mark.parametrize("B", [257, 1024, 4096])
+def test_fp16_persistent_trunk(B, fx, monkeypatch):
+    """configs[4]'s fp16 net on the fp16 wino4 convs (conv_algo="wino4"): the stem, tower and
+    heads as one persistent launch per resident chunk (az_trunk_wino4_heads_fp16_gpu) against
+    the per-layer fp16 wino4 launches + the separate heads kernel, bit for bit (repeated
+    launches), and against the reference's nets at configs[4]'s stated bound."""
+    fused = inference_copy(golden_net("az", fx), "cuda", dtype=torch.float16, conv_algo="wino4")
+    assert fused.precision == "fp16" and all(c.algo == "wino4" for c in fused.c1)
+    assert fused._trunk4_fp16_ready(list(fused.c1), list(fused.c2))
+    monkeypatch.setattr(FusedInferenceNet, "trunk_fp16", False)
+    lp, lv = _run(fused, fx["canon"], B)
+    monkeypatch.setattr(FusedInferenceNet, "trunk_fp16", True)
+    for _ in range(3):
+        p, v = _run(fused, fx["canon"], B)
+        assert np.array_equal(p, lp) and np.array_equal(v, lv)
+    wp, wv = _want(fx, "az", B)
+    np.testing.assert_allclose(p, wp, atol=2e-3, rtol=2e-2)
+    np.testing.assert_allclose(v, wv, atol=2e-3, rtol=2e-2)
