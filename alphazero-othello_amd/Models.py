@@ -232,14 +232,20 @@ class _ConvEpilogue(nn.Module):
 
 
 def default_conv_algo(precision, channels):
-    """The 16-bit-pipe 3x3 conv algorithm: "wino" (csrc/conv_wino.hip, Winograd F(2x2,3x3))
-    where it measured faster (split3, 128 channels: profiles/r01_conv_mx.jsonl), "direct"
-    (csrc/conv16.hip) elsewhere; AZ_CONV_ALGO=direct|wino overrides."""
+    """The 16-bit-pipe 3x3 conv algorithm: "wino4" (csrc/conv_wino4.hip) for fp16x2 and, at
+    128 channels, for fp16 (whose leaf evaluation then runs as the persistent fp16 trunk with
+    the stem and heads: 196 against 276 us per B = 1,024 evaluation for the direct fp16 conv,
+    configs[4] 229 against 171 games/s, profiles/r05_c5_conv_algo.json); "wino"
+    (csrc/conv_wino.hip, Winograd F(2x2,3x3)) where it measured faster (split3, 128 channels:
+    profiles/r01_conv_mx.jsonl); "direct" (csrc/conv16.hip) elsewhere.  AZ_CONV_ALGO=
+    direct|wino|wino4 overrides (fp16x2 stays wino4)."""
     if precision == "fp16x2":
         return "wino4"
     env = os.environ.get("AZ_CONV_ALGO")
     if env in ("direct", "wino", "wino4"):
         return "wino" if env == "wino4" and channels != 128 else env
+    if precision == "fp16" and channels == 128:
+        return "wino4"
     return "wino" if precision == "split3" and channels == 128 else "direct"
 
 

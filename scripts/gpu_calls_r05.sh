@@ -578,4 +578,17 @@ c37() {
   exit 0
 }
 
+c38() {
+  # fp16 at 128 channels defaults to the wino4 convs (the persistent fp16 trunk): the whole GPU
+  # suite, smoke(), configs[4] and configs[2] bench lines
+  export OUT=gpurun_out/r05ao
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench_c5 400 python bench.py --workload c5 || exit $?
+  run bench 600 python bench.py
+  exit 0
+}
+
 "$@"
