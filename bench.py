@@ -439,10 +439,15 @@ def trunk_roofline(sp, device, n_boards):
     launch stream at the bench's leaf batch.  achieved = the block convs' MFMA FLOP per launch
     (2*B*64*C*C*9 algorithmic per conv x 16/36 Winograd x 3 fp16x2 products) / the average
     launch time, against the dense fp16 MFMA peak; the stem and heads (< 1 % of the FLOP) are
-    inside the time but not counted."""
+    inside the time but not counted.  configs[4]'s fp16 net runs the same launch in fp16
+    (az_trunk_wino4_heads_fp16_gpu: one product); above 4 x CUs boards the evaluation is one
+    launch per resident chunk and the time is the evaluation's."""
     net = sp.net
-    if not (hasattr(net, "c1") and getattr(net, "conv_impl", "") == "hip" and net.c1
-            and all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16x2"
+    if not (hasattr(net, "c1") and getattr(net, "conv_impl", "") == "hip" and net.c1):
+        return None
+    prec = net.c1[0].precision
+    if not (prec in ("fp16x2", "fp16")
+            and all(getattr(c, "algo", "") == "wino4" and c.precision == prec
                     for c in list(net.c1) + list(net.c2))):
         return None
     C, n_convs = net.c1[0].channels, 2 * len(net.c1)
@@ -456,7 +461,7 @@ def trunk_roofline(sp, device, n_boards):
         torch.cuda.synchronize()
         ms = launch_ms(lambda: net.evaluate_into(x, pr, va), 50)
     flop = 2.0 * n_boards * 64 * C * C * 9 * n_convs
-    mult = 3 * 256 / 576
+    mult = (3 if prec == "fp16x2" else 1) * 256 / 576
     executed = mult * flop / (ms * 1e-3) / 1e12
     # the whole net's algorithmic FLOP per evaluation (189.0 MFLOP for
     # AlphaZeroNet(5x128)): stem 3x3 (1 -> C), the block convs, the 1x1 policy (2) + value (1)
@@ -466,14 +471,17 @@ def trunk_roofline(sp, device, n_boards):
     algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
     traffic = None  # HBM bytes per launch, PMC (scripts/gpu_calls_r05.sh c23), at B = 1,024
     tj = os.path.join(ROOT, "profiles", "trunk_traffic.json")
-    if n_boards == 1024 and os.path.exists(tj):
+    if n_boards == 1024 and prec == "fp16x2" and os.path.exists(tj):
         try:
             traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    return {"kernel": "k_trunk_wino4 (az_trunk_wino4_heads_gpu: stem + %d block convs, Winograd "
-                      "F(2x2,3x3) fp16x2, two boards per workgroup, each layer's input resident "
-                      "in LDS, + heads)" % n_convs,
+    fn = "az_trunk_wino4_heads_gpu" if prec == "fp16x2" else "az_trunk_wino4_heads_fp16_gpu"
+    cap = net._trunk4_cap(device)
+    return {"kernel": "k_trunk_wino4 (%s: stem + %d block convs, Winograd F(2x2,3x3) %s, two "
+                      "boards per workgroup, each layer's input resident in LDS, + heads)"
+                      % (fn, n_convs, prec),
+            "launches_per_evaluation": -(-n_boards // cap),
             "bound": "mfma", "achieved": round(algorithmic, 1), "peak": MFMA16_PEAK,
             "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": traffic,
             "achieved_basis": "algorithmic: the net's %.1f MFLOP per evaluation x boards / launch "
@@ -931,10 +939,9 @@ def main():
             and getattr(sp.net, "conv_impl", "") == "hip":
         lb = a.games // a.pipelines * a.leaves  # one evaluation's boards
         result["roofline_conv"] = conv_roofline(sp, device, lb)
-        if lb <= 4 * torch.cuda.get_device_properties(device).multi_processor_count:
-            rt = trunk_roofline(sp, device, lb)
-            if rt is not None:
-                result["roofline_trunk"] = rt
+        rt = trunk_roofline(sp, device, lb)  # above 4 x CUs boards: one launch per chunk
+        if rt is not None:
+            result["roofline_trunk"] = rt
     if rank == 0 and not a.skip_cpu:
         result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds,
                                                    a.cpu_workers or host_cpu_share())
