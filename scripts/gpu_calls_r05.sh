@@ -591,4 +591,17 @@ c38() {
   exit 0
 }
 
+c39() {
+  # configs[4] and configs[3] lines with roofline_trunk (fp16 trunk; chunked evaluations), and
+  # configs[4]'s kernel profile
+  export OUT=gpurun_out/r05ap
+  mkdir -p $OUT
+  run bench_c5 400 python bench.py --workload c5 || exit $?
+  run bench_c4 400 python bench.py --workload c4 --skip-cpu || exit $?
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c5 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --workload c5 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  exit 0
+}
+
 "$@"
