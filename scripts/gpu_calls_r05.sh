@@ -604,4 +604,14 @@ c39() {
   exit 0
 }
 
+c40() {
+  # configs[1] (FastOthelloNet, 4,096 games, 100 sims): kernel profile
+  export OUT=gpurun_out/r05ar
+  mkdir -p $OUT
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 2000 --warmup 4000
+  exit 0
+}
+
 "$@"
