@@ -610,7 +610,8 @@ c40() {
   mkdir -p $OUT
   export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
   run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
-    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 2000 --warmup 4000
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
   exit 0
 }
 
