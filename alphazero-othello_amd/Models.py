@@ -808,6 +808,32 @@ class FusedInferenceNet(nn.Module, Inference):
             }
         return True
 
+    # AZ_FAST_HEADS (default on): FastOthelloNet's heads as ONE GEMM of the tail output, read in
+    # its NHWC layout (no flattening copy: the FC weights' columns are permuted instead),
+    # against [fc_policy; fc_value1], then az_heads_fast_finish_gpu (softmax, ReLU -> fc_value2
+    # -> tanh) straight into the engine's buffers -- instead of a flattening copy, three GEMMs,
+    # softmax / ReLU / tanh kernels and two device copies per evaluation
+    fuse_fast_heads = os.environ.get("AZ_FAST_HEADS", "1") == "1"
+
+    def _fast_heads_ready(self):
+        if not (self.kind == "fast" and self.conv_impl == "hip" and self.fuse_fast_heads):
+            return False
+        if not hasattr(self, "_fw"):
+            pol, v1, v2 = self.fc_policy, self.fc_value1, self.fc_value2
+            w = torch.cat([pol.weight.detach(), v1.weight.detach()]).float()  # [129, C * 64]
+            n_out, C = w.shape[0], w.shape[1] // 64
+            # reference flattening index c * 64 + square -> the NHWC tail's square * C + c
+            w = w.view(n_out, C, 64).permute(0, 2, 1).reshape(n_out, 64 * C)
+            ld = 132  # logits row stride (columns 129.. are zero)
+            wt = torch.zeros(64 * C, ld, dtype=torch.float32, device=w.device)
+            wt[:, :n_out] = w.t()
+            bias = torch.zeros(ld, dtype=torch.float32, device=w.device)
+            bias[:n_out] = torch.cat([pol.bias.detach(), v1.bias.detach()]).float()
+            self._fw = {"wt": wt.contiguous(), "bias": bias, "ld": ld,
+                        "w2": v2.weight.detach().float().reshape(-1).contiguous(),
+                        "b2": v2.bias.detach().float().contiguous()}
+        return True
+
     def evaluate_into(self, planes, priors, values, stem_done=False):
         """Leaf evaluation straight into the engine's buffers: priors float32 [B, 65]
         (softmax), values float32 [B] (tanh).  AlphaZeroNet on the HIP trunk runs both heads
@@ -815,6 +841,18 @@ class FusedInferenceNet(nn.Module, Inference):
         the engine has run the stem into engine_stem's buffers (planes are then not read)."""
         if stem_done and not self._fused_heads_ready():
             raise RuntimeError("stem_done on a net without an engine stem")
+        if self._fast_heads_ready():
+            import az_native as nat
+
+            B = planes.shape[0]
+            fw = self._fw
+            t = self.tail(self._trunk(planes.view(B, 1, 8, 8)))
+            hf = t.permute(0, 2, 3, 1).reshape(B, -1)  # a view of the channels-last output
+            logits = torch.addmm(fw["bias"], hf, fw["wt"])
+            nat.check(nat.lib.az_heads_fast_finish_gpu(
+                nat.ptr(logits), fw["ld"], nat.ptr(fw["w2"]), nat.ptr(fw["b2"]), nat.ptr(priors),
+                nat.ptr(values), B, nat.stream_ptr()), "az_heads_fast_finish_gpu")
+            return
         if not self._fused_heads_ready():
             p, v = self.evaluate_planes(planes)
             priors.copy_(p)
@@ -835,7 +873,7 @@ class FusedInferenceNet(nn.Module, Inference):
             "az_heads_az_gpu")
 
     def evaluate_planes(self, planes):
-        if not self._fused_heads_ready():
+        if not (self._fused_heads_ready() or self._fast_heads_ready()):
             return Inference.evaluate_planes(self, planes)
         B = planes.shape[0]
         pr = torch.empty(B, 65, dtype=torch.float32, device=planes.device)

@@ -65,3 +65,55 @@ extern "C" int az_heads_az_gpu(const float* h, const float* wpv, const float* bp
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
+
+// FastOthelloNet's heads after their two input GEMMs (reference Models.py:106-112 + the
+// softmax of MCTS_model.py:319): the host runs ONE GEMM of the flattened tail output against
+// [fc_policy; fc_value1] (logits [n][ld], columns 0..64 the policy logits, 65..128 the value
+// hidden layer before its ReLU); this kernel finishes both heads per board -- softmax over the
+// 65 logits into priors, tanh(b2 + sum_j w2[j] relu(hidden_j)) into values.  One wavefront per
+// board, lane j holds logit j (lane 0 also logit 64) and hidden unit j.
+namespace {
+__global__ __launch_bounds__(256) void k_heads_fast_finish(const float* __restrict__ logits,
+                                                           int ld,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ b2,
+                                                           float* __restrict__ priors,
+                                                           float* __restrict__ values,
+                                                           int n_boards) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n_boards) return;  // wave-uniform
+  const float* row = logits + (size_t)b * ld;
+  const float l0 = row[lane], l64 = row[64], hid = row[65 + lane];
+  float m = fmaxf(l0, l64);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  const float e0 = expf(l0 - m), e64 = expf(l64 - m);
+  float s = e0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  s += e64;
+  float* pr = priors + (size_t)b * 65;
+  pr[lane] = e0 / s;
+  if (lane == 0) pr[64] = e64 / s;
+  float v = fmaxf(hid, 0.0f) * w2[lane];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) values[b] = tanhf(v + b2[0]);
+}
+}  // namespace
+
+extern "C" int az_heads_fast_finish_gpu(const float* logits, int32_t ld, const float* w2,
+                                        const float* b2, float* priors, float* values,
+                                        int32_t n_boards, void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && ld >= 129, AZ_ERR_ARG,
+             "az_heads_fast_finish_gpu: n_boards %d < 0 or ld %d < 129", n_boards, ld);
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(logits && w2 && b2 && priors && values, AZ_ERR_ARG,
+             "az_heads_fast_finish_gpu: null buffer");
+  const unsigned grid = (unsigned)((n_boards + 3) / 4);
+  hipLaunchKernelGGL(k_heads_fast_finish, dim3(grid), dim3(256), 0, azc::as_stream(stream),
+                     logits, (int)ld, w2, b2, priors, values, (int)n_boards);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}

@@ -124,3 +124,22 @@ def test_fp16_persistent_trunk(B, fx, monkeypatch):
     wp, wv = _want(fx, "az", B)
     np.testing.assert_allclose(p, wp, atol=2e-3, rtol=2e-2)
     np.testing.assert_allclose(v, wv, atol=2e-3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B", [1, 33, 4096])
+def test_fast_fused_heads(B, fx, monkeypatch):
+    """FastOthelloNet's heads as one GEMM on the NHWC tail output + az_heads_fast_finish_gpu
+    (bench --workload c2's path) against the module's own heads (flattening copy, three
+    GEMMs, softmax / ReLU / tanh) and the reference's nets."""
+    fused = inference_copy(golden_net("fast", fx), "cuda")
+    assert fused._fast_heads_ready()
+    monkeypatch.setattr(FusedInferenceNet, "fuse_fast_heads", False)
+    up, uv = _run(fused, fx["canon"], B)
+    monkeypatch.setattr(FusedInferenceNet, "fuse_fast_heads", True)
+    p, v = _run(fused, fx["canon"], B)
+    assert np.isfinite(p).all() and np.isfinite(v).all()
+    np.testing.assert_allclose(p, up, atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(v, uv, atol=1e-6, rtol=1e-5)
+    wp, wv = _want(fx, "fast", B)
+    np.testing.assert_allclose(p, wp, atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(v, wv, atol=1e-5, rtol=1e-4)
