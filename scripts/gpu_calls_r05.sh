@@ -633,4 +633,22 @@ c41() {
   exit 0
 }
 
+c42() {
+  # FastOthelloNet heads GEMM in nn.Linear's weight layout; configs[1] with the Winograd split3
+  # convs at 64 channels
+  export OUT=gpurun_out/r05at
+  mkdir -p $OUT
+  run pytest_fast 400 python -u -m pytest tests/test_net_golden_gpu.py -m gpu -x -v -p no:cacheprovider \
+    --timeout 300 --timeout-method thread -k "fast" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_wino 300 env AZ_CONV_ALGO=wino python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
+
 "$@"
