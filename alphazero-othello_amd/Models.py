@@ -824,14 +824,19 @@ class FusedInferenceNet(nn.Module, Inference):
             n_out, C = w.shape[0], w.shape[1] // 64
             # reference flattening index c * 64 + square -> the NHWC tail's square * C + c
             w = w.view(n_out, C, 64).permute(0, 2, 1).reshape(n_out, 64 * C)
-            ld = 132  # logits row stride (rows 129.. of the weight are zero)
-            # [ld][C * 64] as nn.Linear keeps it (F.linear: hipBLASLt's transposed-B GEMM, 53.3
-            # -> %s us per 2,048-board evaluation against the [C * 64][ld] layout)
-            wt = torch.zeros(ld, 64 * C, dtype=torch.float32, device=w.device)
-            wt[:n_out] = w
+            ld = 132  # logits row stride (columns 129.. are zero)
+            wt = torch.zeros(64 * C, ld, dtype=torch.float32, device=w.device)
+            wt[:, :n_out] = w.t()
             bias = torch.zeros(ld, dtype=torch.float32, device=w.device)
             bias[:n_out] = torch.cat([pol.bias.detach(), v1.bias.detach()]).float()
-            self._fw = {"wt": wt.contiguous(), "bias": bias, "ld": ld,
+            # split-K (AZ_FAST_SPLITK, default 4): the GEMM's 2,048 x 132 output alone is too few
+            # tiles for the chip; S slices of the reduction as one batched GEMM, the partial
+            # sums added in slice order by the finish kernel
+            S = int(os.environ.get("AZ_FAST_SPLITK", "4"))
+            if S < 1 or (64 * C) % S:
+                raise ValueError(f"AZ_FAST_SPLITK={S} does not divide the {64 * C} inputs")
+            self._fw = {"wk": wt.contiguous().view(S, 64 * C // S, ld), "S": S,
+                        "bias": bias, "ld": ld,
                         "w2": v2.weight.detach().float().reshape(-1).contiguous(),
                         "b2": v2.bias.detach().float().contiguous()}
         return True
@@ -850,10 +855,12 @@ class FusedInferenceNet(nn.Module, Inference):
             fw = self._fw
             t = self.tail(self._trunk(planes.view(B, 1, 8, 8)))
             hf = t.permute(0, 2, 3, 1).reshape(B, -1)  # a view of the channels-last output
-            logits = F.linear(hf, fw["wt"], fw["bias"])
+            S = fw["S"]
+            part = torch.bmm(hf.view(B, S, -1).transpose(0, 1), fw["wk"])  # [S, B, ld]
             nat.check(nat.lib.az_heads_fast_finish_gpu(
-                nat.ptr(logits), fw["ld"], nat.ptr(fw["w2"]), nat.ptr(fw["b2"]), nat.ptr(priors),
-                nat.ptr(values), B, nat.stream_ptr()), "az_heads_fast_finish_gpu")
+                nat.ptr(part), fw["ld"], S, nat.ptr(fw["bias"]), nat.ptr(fw["w2"]),
+                nat.ptr(fw["b2"]), nat.ptr(priors), nat.ptr(values), B, nat.stream_ptr()),
+                "az_heads_fast_finish_gpu")
             return
         if not self._fused_heads_ready():
             p, v = self.evaluate_planes(planes)

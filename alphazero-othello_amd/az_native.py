@@ -133,7 +133,7 @@ SIGNATURES = {
     "az_trunk_wino4_heads_gpu": [_P] * 11 + [_I32] * 3 + [_P] * 10 + [_P],
     "az_trunk_wino4_heads_fp16_gpu": [_P] * 11 + [_I32] * 3 + [_P] * 10 + [_P],
     "az_heads_az_gpu": [_P] * 11 + [_I32, _I32, _P],
-    "az_heads_fast_finish_gpu": [_P, _I32, _P, _P, _P, _P, _I32, _P],
+    "az_heads_fast_finish_gpu": [_P, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P],
     "az_conv3x3_mx_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_stem_gpu": [_P] * 7 + [_I32, _I32, _I32, _I32, _P],
     "az_replay_aggregate_gpu": [_P] * 5 + [_I64] + [_P] * 10,

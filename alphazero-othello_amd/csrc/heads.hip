@@ -68,13 +68,17 @@ extern "C" int az_heads_az_gpu(const float* h, const float* wpv, const float* bp
 
 // FastOthelloNet's heads after their two input GEMMs (reference Models.py:106-112 + the
 // softmax of MCTS_model.py:319): the host runs ONE GEMM of the flattened tail output against
-// [fc_policy; fc_value1] (logits [n][ld], columns 0..64 the policy logits, 65..128 the value
-// hidden layer before its ReLU); this kernel finishes both heads per board -- softmax over the
-// 65 logits into priors, tanh(b2 + sum_j w2[j] relu(hidden_j)) into values.  One wavefront per
-// board, lane j holds logit j (lane 0 also logit 64) and hidden unit j.
+// [fc_policy; fc_value1], split over `parts` slices of the reduction (part p: logits partial
+// sums [n][ld] at p * part_stride; columns 0..64 the policy logits, 65..128 the value hidden
+// layer before its ReLU); this kernel adds the parts in order and the bias, then finishes both
+// heads per board -- softmax over the 65 logits into priors, tanh(b2 + sum_j w2[j]
+// relu(hidden_j)) into values.  One wavefront per board, lane j holds logit j (lane 0 also
+// logit 64) and hidden unit j.
 namespace {
 __global__ __launch_bounds__(256) void k_heads_fast_finish(const float* __restrict__ logits,
-                                                           int ld,
+                                                           int ld, int parts,
+                                                           long long part_stride,
+                                                           const float* __restrict__ bias,
                                                            const float* __restrict__ w2,
                                                            const float* __restrict__ b2,
                                                            float* __restrict__ priors,
@@ -84,7 +88,16 @@ __global__ __launch_bounds__(256) void k_heads_fast_finish(const float* __restri
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= n_boards) return;  // wave-uniform
   const float* row = logits + (size_t)b * ld;
-  const float l0 = row[lane], l64 = row[64], hid = row[65 + lane];
+  float l0 = row[lane], l64 = row[64], hid = row[65 + lane];
+  for (int p = 1; p < parts; ++p) {
+    const float* r = row + p * part_stride;
+    l0 += r[lane];
+    l64 += r[64];
+    hid += r[65 + lane];
+  }
+  l0 += bias[lane];
+  l64 += bias[64];
+  hid += bias[65 + lane];
   float m = fmaxf(l0, l64);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
@@ -103,17 +116,20 @@ __global__ __launch_bounds__(256) void k_heads_fast_finish(const float* __restri
 }
 }  // namespace
 
-extern "C" int az_heads_fast_finish_gpu(const float* logits, int32_t ld, const float* w2,
-                                        const float* b2, float* priors, float* values,
-                                        int32_t n_boards, void* stream) {
-  AZ_REQUIRE(n_boards >= 0 && ld >= 129, AZ_ERR_ARG,
-             "az_heads_fast_finish_gpu: n_boards %d < 0 or ld %d < 129", n_boards, ld);
+extern "C" int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t parts,
+                                        const float* bias, const float* w2, const float* b2,
+                                        float* priors, float* values, int32_t n_boards,
+                                        void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && ld >= 129 && parts >= 1, AZ_ERR_ARG,
+             "az_heads_fast_finish_gpu: n_boards %d < 0, ld %d < 129 or parts %d < 1", n_boards,
+             ld, parts);
   if (n_boards == 0) return AZ_OK;
-  AZ_REQUIRE(logits && w2 && b2 && priors && values, AZ_ERR_ARG,
+  AZ_REQUIRE(logits && bias && w2 && b2 && priors && values, AZ_ERR_ARG,
              "az_heads_fast_finish_gpu: null buffer");
   const unsigned grid = (unsigned)((n_boards + 3) / 4);
   hipLaunchKernelGGL(k_heads_fast_finish, dim3(grid), dim3(256), 0, azc::as_stream(stream),
-                     logits, (int)ld, w2, b2, priors, values, (int)n_boards);
+                     logits, (int)ld, (int)parts, (long long)n_boards * ld, bias, w2, b2, priors,
+                     values, (int)n_boards);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

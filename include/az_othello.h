@@ -523,12 +523,14 @@ int az_heads_az_gpu(const float* h, const float* wpv, const float* bpv, const fl
                     int32_t channels, void* stream);
 
 /* FastOthelloNet's heads after their input GEMMs (reference Models.py:106-112, softmax of
- * MCTS_model.py:319): logits float [n_boards][ld] (ld >= 129) = the flattened tail output x
- * [fc_policy; fc_value1]^T + biases (columns 0..64 policy logits, 65..128 the value hidden
- * layer before its ReLU); w2 [64], b2 [1] = fc_value2.  Writes priors [n_boards][65]
- * (softmax) and values [n_boards] (tanh). */
-int az_heads_fast_finish_gpu(const float* logits, int32_t ld, const float* w2, const float* b2,
-                             float* priors, float* values, int32_t n_boards, void* stream);
+ * MCTS_model.py:319): logits float [parts][n_boards][ld] (ld >= 129) = the flattened tail
+ * output x [fc_policy; fc_value1]^T split over `parts` slices of the reduction (columns 0..64
+ * policy logits, 65..128 the value hidden layer before its ReLU), summed here in part order,
+ * then + bias [129]; w2 [64], b2 [1] = fc_value2.  Writes priors [n_boards][65] (softmax) and
+ * values [n_boards] (tanh). */
+int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t parts, const float* bias,
+                             const float* w2, const float* b2, float* priors, float* values,
+                             int32_t n_boards, void* stream);
 
 /* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
  * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,

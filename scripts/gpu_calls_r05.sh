@@ -651,4 +651,22 @@ c42() {
   exit 0
 }
 
+c43() {
+  # FastOthelloNet heads GEMM split over the reduction (AZ_FAST_SPLITK 1 / 4 / 8)
+  export OUT=gpurun_out/r05au
+  mkdir -p $OUT
+  run pytest_fast 400 python -u -m pytest tests/test_net_golden_gpu.py tests/test_pipelined_gpu.py -m gpu -x -v \
+    -p no:cacheprovider --timeout 300 --timeout-method thread -k "fast" || exit $?
+  for i in 1 2; do
+    run bench_c2_s4 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_s1 300 env AZ_FAST_SPLITK=1 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_s8 300 env AZ_FAST_SPLITK=8 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
+
 "$@"
