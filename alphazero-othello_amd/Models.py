@@ -829,10 +829,11 @@ class FusedInferenceNet(nn.Module, Inference):
             wt[:, :n_out] = w.t()
             bias = torch.zeros(ld, dtype=torch.float32, device=w.device)
             bias[:n_out] = torch.cat([pol.bias.detach(), v1.bias.detach()]).float()
-            # split-K (AZ_FAST_SPLITK, default 4): the GEMM's 2,048 x 132 output alone is too few
-            # tiles for the chip; S slices of the reduction as one batched GEMM, the partial
-            # sums added in slice order by the finish kernel
-            S = int(os.environ.get("AZ_FAST_SPLITK", "4"))
+            # split-K (AZ_FAST_SPLITK, experiments): S slices of the reduction as one batched
+            # GEMM, the partial sums added in slice order by the finish kernel.  S = 4 cut the
+            # GEMM + finish kernels 61.6 -> 53.6 us per 2,048 boards, but configs[1] ran 1,970-1,985
+            # games/s against 2,018-2,025 with S = 1 (8: 1,844; profiles/r05_fast_heads_ab.json)
+            S = int(os.environ.get("AZ_FAST_SPLITK", "1"))
             if S < 1 or (64 * C) % S:
                 raise ValueError(f"AZ_FAST_SPLITK={S} does not divide the {64 * C} inputs")
             self._fw = {"wk": wt.contiguous().view(S, 64 * C // S, ld), "S": S,
