@@ -669,4 +669,17 @@ c43() {
   exit 0
 }
 
+c44() {
+  # the final tree (fp16 persistent trunk default, FastOthelloNet fused heads): the whole GPU
+  # suite, smoke(), the default bench line and the configs[1] line
+  export OUT=gpurun_out/r05av
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench 600 python bench.py || exit $?
+  run bench_c2 400 python bench.py --workload c2 || exit $?
+  exit 0
+}
+
 "$@"
