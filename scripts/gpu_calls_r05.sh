@@ -682,4 +682,16 @@ c44() {
   exit 0
 }
 
+c45() {
+  # configs[1] with the fused fast heads: 1 / 2 / 4 pipelines
+  export OUT=gpurun_out/r05aw
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_c2_p2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_p4 300 python bench.py --workload c2 --skip-cpu --skip-kernel --pipelines 4 || exit $?
+    run bench_c2_p1 300 python bench.py --workload c2 --skip-cpu --skip-kernel --pipelines 1 || exit $?
+  done
+  exit 0
+}
+
 "$@"
