@@ -43,10 +43,22 @@ def get_training_data(trajectory, winning_player, lambd: float = 1.0):
 _BATCH = {"key": None, "games": []}
 
 
-def _dropin_batch_size():
+def _dropin_batch_size(args=None):
+    """AZ_DROPIN_BATCH (default 32), capped at this worker's share of the generation when
+    the args carry train.py's num_self_play / num_workers (train.py:413, 420): with the
+    reference's 300 games over os.cpu_count() workers a worker plays ceil(300 / workers)
+    games per batch instead of 32 it would mostly discard."""
     import os
 
-    return int(os.environ.get("AZ_DROPIN_BATCH", "32"))
+    n = int(os.environ.get("AZ_DROPIN_BATCH", "32"))
+    args = args or {}
+    try:
+        games, workers = int(args["num_self_play"]), int(args["num_workers"])
+    except (KeyError, TypeError, ValueError):
+        return n
+    if n > 1 and games > 0 and workers > 0:
+        n = min(n, -(-games // workers))
+    return n
 
 
 def _batch_key(board_size, args, policy_state):
@@ -65,9 +77,13 @@ def _batch_key(board_size, args, policy_state):
 
 
 def _games_from_rows(rows):
-    """Engine sample rows -> one list of reference tuples per game.  A game's rows are
-    contiguous in the sample ring (finish_game reserves them at once) and each starts at the
-    initial position, the only position with four stones."""
+    """Engine sample rows -> one list of reference tuples per game, in SLOT order.  A game's
+    rows are contiguous in the sample ring (finish_game reserves them at once) and each starts
+    at the initial position, the only position with four stones.  The ring itself is in
+    completion order -- all of a batch's games start together, so that is game-length order --
+    and handing games out in it would return the shortest games first; a slot plays one
+    game of the batch from its own Philox stream, so slot order does not depend on the
+    outcome (games of one slot keep their ring order)."""
     own = np.asarray(rows["own"]).view(np.uint64)
     opp = np.asarray(rows["opp"]).view(np.uint64)
     occ = own | opp
@@ -76,7 +92,11 @@ def _games_from_rows(rows):
         stones += ((occ >> np.uint64(sh)) & np.uint64(1)).astype(np.int64)
     starts = list(np.flatnonzero(stones == 4)) + [len(own)]
     tuples = _rows_to_tuples(rows)
-    return [tuples[a:b] for a, b in zip(starts[:-1], starts[1:])]
+    games = [tuples[a:b] for a, b in zip(starts[:-1], starts[1:])]
+    if "slot" in rows and len(games):
+        slot = np.asarray(rows["slot"])[np.asarray(starts[:-1])]
+        games = [games[i] for i in np.argsort(slot, kind="stable")]
+    return games
 
 
 @torch.no_grad()
@@ -84,18 +104,20 @@ def one_self_play(args_tuple):
     """One complete game (self_play_worker.py:38-88); returns [(state, pi, G)].
 
     train.py's spawn pool (train.py:199-225) calls this once per game in each worker
-    process.  By default (AZ_DROPIN_BATCH = 32) the worker's first call plays that many
-    games at once on the batched GPU engine (BatchedSelfPlay: the same search, K =
+    process.  By default (AZ_DROPIN_BATCH = 32, capped at the worker's share
+    ceil(num_self_play / num_workers) when args carry them) the worker's first call plays that
+    many games at once on the batched GPU engine (BatchedSelfPlay: the same search, K =
     args['num_threads'] virtual-loss leaves per step, Dirichlet root noise, temperature
     schedule and TD(lambda) targets; its Philox seed drawn from np.random, which the pool's
     _worker_init seeds) and hands them out one per call while the policy weights and args
-    are unchanged -- games distributed like the reference's, the engine's rate instead of
+    are unchanged, in slot order (independent of the games' lengths and outcomes:
+    _games_from_rows) -- games distributed like the reference's, the engine's rate instead of
     one search at a time.  AZ_DROPIN_BATCH <= 1: one game per call through the drop-in MCTS
     (np.random draws in the reference's order)."""
-    n = _dropin_batch_size()
-    if n <= 1:
-        return _one_game(args_tuple)
     board_size, args, policy_state, _ = args_tuple
+    if _dropin_batch_size() <= 1:
+        return _one_game(args_tuple)
+    n = _dropin_batch_size(args)
     assert board_size == 8
     key = _batch_key(board_size, args, policy_state)
     if _BATCH["key"] != key:

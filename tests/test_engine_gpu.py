@@ -314,12 +314,8 @@ def test_drop_in_one_self_play_batched(monkeypatch):
     want = spw._games_from_rows(spw._local_rows(net, args, 4, None, seed, 0, False,
                                                 torch.float32))
     assert len(want) == 4
-    # the sample ring records games in completion order: compare as sets of games
+    # handed out in slot order (_games_from_rows), exactly the engine's games
 
-    def gkey(game):
-        return b"".join(s.tobytes() + pi.tobytes() + np.float64(z).tobytes() for s, pi, z in game)
-
-    got, want = sorted(got, key=gkey), sorted(want, key=gkey)
     for g, w in zip(got, want):
         assert len(g) == len(w) >= 10
         s0 = g[0][0]
@@ -338,3 +334,40 @@ def test_drop_in_one_self_play_batched(monkeypatch):
     assert spw._BATCH["key"] != key and len(spw._BATCH["games"]) == 3
     spw.one_self_play((8, dict(args, num_simulations=7), ps2, None))
     assert len(spw._BATCH["games"]) == 3
+
+
+def test_drop_in_batch_hands_out_slot_order(monkeypatch):
+    """AZ_DROPIN_BATCH = 8: the first k games one_self_play returns are exactly slots
+    0..k-1's games of the batch (not the k that finished first: the sample ring is in
+    completion order, i.e. shortest first), so a worker returning only part of its batch
+    returns games whose lengths do not depend on the handout."""
+    import self_play_worker as spw
+    from Models import FastOthelloNet
+
+    monkeypatch.setenv("AZ_DROPIN_BATCH", "8")
+    spw._BATCH.update(key=None, games=[])
+    torch.manual_seed(0)
+    net = FastOthelloNet(8, 65)
+    ps = (FastOthelloNet, net.get_config(), net.state_dict())
+    args = {"c_puct": 2.0, "num_simulations": 6, "dirichlet_alpha": 1.0,
+            "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
+            "lambda": 0.98}
+    np.random.seed(7)
+    got = [spw.one_self_play((8, args, ps, None)) for _ in range(3)]
+    np.random.seed(7)
+    seed = int(np.random.randint(0, 2**31 - 1))
+    rows = spw._local_rows(net, args, 8, None, seed, 0, False, torch.float32)
+    slot = np.asarray(rows["slot"])
+    tuples = spw._rows_to_tuples(rows)
+    per_slot = [[tuples[i] for i in np.flatnonzero(slot == s)] for s in range(8)]
+    assert sorted(len(g) for g in per_slot) == sorted(len(g) for g in spw._games_from_rows(rows))
+    for k, g in enumerate(got):
+        w = per_slot[k]
+        assert len(g) == len(w)
+        for (s, pi, z), (ws, wpi, wz) in zip(g, w):
+            assert np.array_equal(s, ws) and np.array_equal(pi, wpi) and z == wz
+    # the ring's completion order differs from slot order for this seed (else the test
+    # would not tell them apart)
+    ring_first = [int(x) for x in slot[np.r_[0, np.flatnonzero(np.diff(slot)) + 1]]]
+    assert ring_first != list(range(8))
+    spw._BATCH.update(key=None, games=[])
