@@ -166,8 +166,8 @@ def inference_copy(net: nn.Module, device, dtype=torch.float32, fused=True,
       "fp32":  fp32 MFMA (csrc/conv.hip);
       "fp16x2": fp32-accurate with half of split3's products: both operands as an fp16
                hi + lo pair after exact power-of-two scaling (per layer for the weights, per
-               board for the inputs), three products in fp32 (csrc/conv_wino4.hip, 128
-               channels; 64-channel convs fall back to split3) -- the default for fp32;
+               board for the inputs), three products in fp32 (csrc/conv_wino4.hip at 128
+               channels, csrc/conv16.hip's direct kernel at 64) -- the default for fp32;
       "fp16":  fp16 operands, fp32 accumulation (config #5's fp16 inference; the default
                when dtype is float16).
     Activations, the stem and the heads stay fp32 on the fused path.  conv_algo ("direct" /
@@ -266,24 +266,27 @@ class _HipConv3x3(nn.Module):
         co, ci = w.shape[0], w.shape[1]
         assert co == ci and co in (64, 128) and w.shape[2:] == (3, 3)
         self.channels = co
-        if precision == "fp16x2" and co != 128:  # the scaled fp16 pair is a wino4 mode
-            precision = "split3"
+        if precision == "fp16x2" and co != 128 and os.environ.get("AZ_CONV64_SPLIT3") == "1":
+            precision = "split3"  # A/B: the bf16x3 direct kernel at 64 channels (round 5's)
         self.precision = precision
         self.algo = "direct" if precision == "fp32" else (algo or default_conv_algo(precision, co))
         if self.algo == "wino4" and co != 128:  # the 4-board form is built for 128 channels
             self.algo = "wino"
+        if precision == "fp16x2" and co != 128:
+            # the scaled fp16 pair at 64 channels: the direct kernel (csrc/conv16.hip), each
+            # workgroup scaling its board by the max |x| it stages
+            self.algo = "direct"
         w9 = w.float().permute(2, 3, 0, 1).reshape(9, co, ci).contiguous()
         self.bias = nn.Parameter(conv.bias.detach().float().contiguous(), requires_grad=False)
         if precision == "fp32":
             self.w9 = nn.Parameter(w9, requires_grad=False)
         else:
             self.mode = self.MODES[precision]
-            planes = 3 if precision == "split3" else 1
             wino = self.algo in ("wino", "wino4")
-            taps = 16 if wino else 9
-            n16 = taps * co * ci * planes
             if wino:
                 n16 = nat.lib.az_conv3x3_wino_prep_bytes(co, self.mode) // 2
+            else:
+                n16 = nat.lib.az_conv3x3_mx_prep_bytes(co, self.mode) // 2
             wq = torch.empty(n16, dtype=torch.int16, device=w.device)
             prep = nat.lib.az_conv3x3_wino_prep_gpu if wino else nat.lib.az_conv3x3_mx_prep_gpu
             nat.check(prep(nat.ptr(w9), nat.ptr(wq), co, self.mode, nat.stream_ptr()),
@@ -639,7 +642,8 @@ class FusedInferenceNet(nn.Module, Inference):
                     return None
                 h = c2(t, res=h, in_absmax=bufs[1], out_absmax=bufs[0], **sk)
             return h
-        elif heads_into is not None and not stem_done and self._trunk4_fp16_ready(c1s, c2s):
+        elif heads_into is not None and not stem_done and \
+                self._trunk4_fp16_ready(c1s, c2s, x.shape[0]):
             # fp16 wino4 convs: the stem, the tower and the heads in one persistent launch
             # per chunk of resident boards (az_trunk_wino4_heads_fp16_gpu)
             B = x.shape[0]
@@ -703,11 +707,15 @@ class FusedInferenceNet(nn.Module, Inference):
     # takes priors / values; 0 = per-layer launches
     trunk_fp16 = os.environ.get("AZ_TRUNK_FP16", "1") == "1"
 
-    def _trunk4_fp16_ready(self, c1s, c2s):
+    def _trunk4_fp16_ready(self, c1s, c2s, B=0):
         convs = c1s + c2s
         if not (self.trunk_fp16 and self.fuse_trunk4 and self.trunk_heads and convs
                 and isinstance(self.stem, _HipStem) and self._fused_heads_ready()
                 and os.environ.get("AZ_W4_BOARDS", "2") == "2"):
+            return False
+        # more boards than are resident at once run one launch per chunk: AZ_TRUNK4_CHUNKS=0
+        # turns that off here as for the fp16x2 trunk (per-layer launches instead)
+        if B > self._trunk4_cap(convs[0].wq.device) and not self.trunk4_chunks:
             return False
         if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16"
                    and c.channels == 128 for c in convs):
@@ -817,6 +825,11 @@ class FusedInferenceNet(nn.Module, Inference):
 
     def _fast_heads_ready(self):
         if not (self.kind == "fast" and self.conv_impl == "hip" and self.fuse_fast_heads):
+            return False
+        # the finish kernel's layout: 65 policy logits + 64 value hidden units per board (one
+        # wavefront per board); any other head shape runs the module heads
+        if not (self.fc_policy.out_features == 65 and self.fc_value1.out_features == 64
+                and self.fc_value2.in_features == 64 and self.fc_value2.out_features == 1):
             return False
         if not hasattr(self, "_fw"):
             pol, v1, v2 = self.fc_policy, self.fc_value1, self.fc_value2

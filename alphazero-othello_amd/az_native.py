@@ -119,6 +119,7 @@ SIGNATURES = {
     "az_conv_stem2_gpu": [_P, _P, _P, _P, _I32, _I32, _P, _P],
     "az_conv3x3_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_prep_gpu": [_P, _P, _I32, _I32, _P],
+    "az_conv3x3_mx_prep_bytes": [_I32, _I32],
     "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_wino_prep_gpu": [_P, _P, _I32, _I32, _P],
     "az_conv3x3_wino_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
@@ -160,6 +161,7 @@ def _load():
         fn.argtypes = args
         fn.restype = _I
     lib.az_conv3x3_wino_prep_bytes.restype = _I64
+    lib.az_conv3x3_mx_prep_bytes.restype = _I64
     return lib
 
 

@@ -12,6 +12,12 @@
 //     (dropped: x1y2, x2y1, x2y2 ~ 2^-24 relative — fp32's own rounding unit).  Six bf16
 //     MFMAs cost 6/16 of one fp32 MFMA of the same shape.
 //   AZ_CONV_FP16: one fp16 product (BASELINE configs[4]'s fp16 inference).
+//   AZ_CONV_FP16X2 (fp32-accurate, half of SPLIT3's products): both operands as an fp16
+//     pair hi + lo (22 significant bits) after exact power-of-two scaling -- the weights per
+//     layer (az_conv3x3_mx_prep_gpu's header), the inputs per board from the board's max |x|,
+//     reduced in the workgroup while it stages the board (no range buffer) -- and the three
+//     leading products lo*hi + hi*lo + hi*hi accumulated in fp32; the epilogue removes both
+//     scales exactly (a power of two).  FastOthelloNet's 64-channel convs (configs[1]).
 //
 // GEMM view: M = B*64 output positions, N = C, K = 9 taps x C.  Workgroup = 1 board
 // (M = 64 rows; 51 KB of LDS: 3 workgroups per CU, so one workgroup's staging and
@@ -51,7 +57,10 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 template <int C_, int MODE_, int BOARDS_ = 2>
 struct Mx {
   static constexpr int C = C_, MODE = MODE_;
-  static constexpr int PLANES = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
+  static constexpr int PLANES = MODE == AZ_CONV_SPLIT3 ? 3 : (MODE == AZ_CONV_FP16X2 ? 2 : 1);
+  static constexpr bool SCALED = MODE == AZ_CONV_FP16X2;  // power-of-two operand scaling
+  // MFMA products per (A, B) fragment pair
+  static constexpr int PRODUCTS = MODE == AZ_CONV_SPLIT3 ? 6 : (MODE == AZ_CONV_FP16X2 ? 3 : 1);
   static constexpr int BOARDS = BOARDS_;
   static constexpr int TM = 2 * BOARDS;             // 32-row tiles per wave (= all rows)
   static constexpr int WAVES = C / 32, THREADS = 64 * WAVES;
@@ -59,6 +68,7 @@ struct Mx {
   static constexpr int A_BYTES = (BOARDS * 64 + 1) * APOS;
   static constexpr int CHUNKS = C / 16, STEPS = 9 * CHUNKS;
   static constexpr int STEP_BYTES = PLANES * C * 32;  // weight bytes per (tap, chunk) step
+  static constexpr int W_BYTES = STEPS * STEP_BYTES;  // the weight words (FP16X2: header after)
   static constexpr size_t LDS_BYTES = A_BYTES;
   static_assert(CHUNKS % 4 == 0, "the chunk loop is unrolled by 4");
 };
@@ -123,6 +133,16 @@ __device__ __forceinline__ void mx_mma(f32x16 (&acc)[G::TM], const AFrag<G>& a,
       for (int mi = 0; mi < G::TM; ++mi)
         acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[PA[t]][mi], b.v[PB[t]], acc[mi],
                                                           0, 0, 0);
+  } else if constexpr (G::MODE == AZ_CONV_FP16X2) {
+    // lo * hi, hi * lo, hi * hi (the lo * lo term is below fp32's rounding unit); consecutive
+    // MFMAs write different accumulators
+    constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi)
+        acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.v[PA[t]][mi], b.v[PB[t]], acc[mi],
+                                                         0, 0, 0);
   } else {
 #pragma unroll
     for (int mi = 0; mi < G::TM; ++mi)
@@ -133,7 +153,7 @@ __device__ __forceinline__ void mx_mma(f32x16 (&acc)[G::TM], const AFrag<G>& a,
 // issue pattern of one main-loop step (see AZ_MX_STEP)
 template <class G>
 __device__ __forceinline__ void mx_sched() {
-  constexpr int kMfma = (G::MODE == AZ_CONV_SPLIT3 ? 6 : 1) * G::TM;
+  constexpr int kMfma = G::PRODUCTS * G::TM;
   constexpr int kDs = G::PLANES * G::TM;
   constexpr int kPer = kMfma / kDs > 0 ? kMfma / kDs : 1;
 #pragma unroll
@@ -194,6 +214,12 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   const int b0 = blockIdx.x * kBoards;
   const int nb = n_boards - b0 < kBoards ? n_boards - b0 : kBoards;
   constexpr int last = G::STEPS - 1;
+  // FP16X2: each staged board's max |x| (float bits: non-negative floats order as unsigned)
+  __shared__ unsigned s_amax[kBoards];
+  if (G::SCALED) {
+    if (tid < kBoards) s_amax[tid] = 0u;
+    __syncthreads();
+  }
 
   // weights of the first three steps are in flight while the boards are staged
   const int wlane = (col0 + r) * 32 + h * 16;
@@ -233,6 +259,37 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
         val[i] = src[v];
       }
     }
+    // FP16X2: the boards' max |x| (this thread's values, then the wave, then LDS), and the
+    // per-board input scale 2^sx[b] that maps it below 2^15 (fp16's max is 65504)
+    float xsc[kBoards];
+    if constexpr (G::SCALED) {
+      unsigned m[kBoards];
+#pragma unroll
+      for (int b = 0; b < kBoards; ++b) m[b] = 0u;
+#pragma unroll
+      for (int i = 0; i < ITER; ++i) {
+        const int v = tid + i * kThreads;
+        const int bb = (v / (C / 4)) >> 6;
+        const unsigned u = max(max(__float_as_uint(fabsf(val[i].x)), __float_as_uint(fabsf(val[i].y))),
+                               max(__float_as_uint(fabsf(val[i].z)), __float_as_uint(fabsf(val[i].w))));
+#pragma unroll
+        for (int b = 0; b < kBoards; ++b)
+          if (bb == b) m[b] = max(m[b], u);
+      }
+#pragma unroll
+      for (int b = 0; b < kBoards; ++b) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m[b] = max(m[b], (unsigned)__shfl_xor((int)m[b], off, 64));
+        if ((tid & 63) == 0) atomicMax(&s_amax[b], m[b]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < kBoards; ++b) {
+        const unsigned mb = s_amax[b];
+        const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;  // max < 2^e
+        xsc[b] = ldexpf(1.0f, 15 - e);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
       const int v = tid + i * kThreads;
@@ -240,7 +297,15 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
       const int pos = v / (C / 4), c4 = v % (C / 4);
       char* dst = lds_a + pos * G::APOS + c4 * 8;
       const f32x4 a = {val[i].x, val[i].y, val[i].z, val[i].w};
-      if constexpr (G::MODE == AZ_CONV_SPLIT3) {
+      if constexpr (G::MODE == AZ_CONV_FP16X2) {
+        // the all-zero position (pos = kBoards * 64) takes board 0's scale: zeros either way
+        const int bb = (pos >> 6) < kBoards ? (pos >> 6) : 0;
+        const f32x4 as = a * xsc[bb];  // exact: a power of two
+        const f16x4 hi = __builtin_convertvector(as, f16x4);
+        const f16x4 lo = __builtin_convertvector(as - __builtin_convertvector(hi, f32x4), f16x4);
+        *reinterpret_cast<f16x4*>(dst) = hi;
+        *reinterpret_cast<f16x4*>(dst + C * 2) = lo;
+      } else if constexpr (G::MODE == AZ_CONV_SPLIT3) {
         const bf16x4 x0 = __builtin_convertvector(a, bf16x4);
         const f32x4 r1 = a - __builtin_convertvector(x0, f32x4);
         const bf16x4 x1 = __builtin_convertvector(r1, bf16x4);
@@ -328,6 +393,19 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   // 32-row tile lies inside one board, so the tail-board test is uniform per tile
   const int co = col0 + r;
   const float bv = bias[co];
+  // FP16X2: 2^-(sx + sw) per tile's board (exact), sw = the weights' scale from the header
+  float osc[G::TM];
+#pragma unroll
+  for (int mi = 0; mi < G::TM; ++mi) osc[mi] = 1.0f;
+  if constexpr (G::SCALED) {
+    const int sw = reinterpret_cast<const int*>(wq + G::W_BYTES)[1];
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi) {
+      const unsigned mb = s_amax[(32 * mi) >> 6];
+      const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;
+      osc[mi] = ldexpf(1.0f, -(15 - e) - sw);
+    }
+  }
   float rv[G::TM][16];
   if (RES && STEM == 2) {  // residual = stem(planes) at (row, co), k_conv_stem's fmaf chain
     float sw[9];
@@ -367,7 +445,7 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
     const size_t o0 = ((size_t)b0 * 64 + 32 * mi + 4 * h) * C + co;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      float v = acc[mi][k] + bv;
+      float v = (G::SCALED ? acc[mi][k] * osc[mi] : acc[mi][k]) + bv;
       if (RES) v += rv[mi][k];
       if (RELU) v = fmaxf(v, 0.0f);
       if (AZ_MX_EXP & 8) {
@@ -379,17 +457,36 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   }
 }
 
-// w9 [9][Co][Ci] fp32 -> wq [9][Ci/16][PLANES][Co][16] 16-bit words
-template <int MODE>
-__global__ void k_conv_mx_prep(const float* __restrict__ w9, uint16_t* __restrict__ wq, int C) {
-  constexpr int P = MODE == AZ_CONV_SPLIT3 ? 3 : 1;
+// w9 [9][Co][Ci] fp32 -> wq [9][Ci/16][PLANES][Co][16] 16-bit words.  FP16X2: w * 2^sw split
+// into an fp16 pair; hdr = the 16-byte header after the words: [0] max |w| bits, [1] sw.
+// With MAXPASS the kernel only reduces max |w| into hdr[0].
+template <int MODE, bool MAXPASS = false>
+__global__ void k_conv_mx_prep(const float* __restrict__ w9, uint16_t* __restrict__ wq, int C,
+                               unsigned* hdr) {
+  constexpr int P = MODE == AZ_CONV_SPLIT3 ? 3 : (MODE == AZ_CONV_FP16X2 ? 2 : 1);
   const int n = 9 * C * C;
+  float wsc = 1.0f;
+  if constexpr (MODE == AZ_CONV_FP16X2 && !MAXPASS) {
+    const unsigned mb = hdr[0];  // max |w| < 2^e
+    const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;
+    wsc = ldexpf(1.0f, 15 - e);  // scaled max < 2^15
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[1] = (unsigned)(15 - e);
+  }
+  unsigned wmax = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int tap = i / (C * C), co = (i / C) % C, ci = i % C;
     const float v = w9[i];
     const size_t base = ((((size_t)tap * (C / 16) + ci / 16) * P) * C + co) * 16 + (ci & 15);
     const size_t pstride = (size_t)C * 16;
-    if constexpr (MODE == AZ_CONV_SPLIT3) {
+    if constexpr (MAXPASS) {
+      wmax = max(wmax, __float_as_uint(fabsf(v)));
+    } else if constexpr (MODE == AZ_CONV_FP16X2) {
+      const float vs = v * wsc;  // exact: a power of two
+      const _Float16 hi = (_Float16)vs;
+      const _Float16 lo = (_Float16)(vs - (float)hi);
+      wq[base] = __builtin_bit_cast(uint16_t, hi);
+      wq[base + pstride] = __builtin_bit_cast(uint16_t, lo);
+    } else if constexpr (MODE == AZ_CONV_SPLIT3) {
       const __bf16 x0 = (__bf16)v;
       const float r1 = v - (float)x0;
       const __bf16 x1 = (__bf16)r1;
@@ -400,6 +497,11 @@ __global__ void k_conv_mx_prep(const float* __restrict__ w9, uint16_t* __restric
     } else {
       wq[base] = __builtin_bit_cast(uint16_t, (_Float16)v);
     }
+  }
+  if constexpr (MAXPASS) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (unsigned)__shfl_xor((int)wmax, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(hdr, wmax);
   }
 }
 
@@ -452,10 +554,15 @@ extern "C" int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channel
   const unsigned grid = (unsigned)((9 * channels * channels + 255) / 256);
   uint16_t* out = static_cast<uint16_t*>(wq);
   if (mode == AZ_CONV_SPLIT3)
-    hipLaunchKernelGGL(k_conv_mx_prep<AZ_CONV_SPLIT3>, dim3(grid), dim3(256), 0, s, w9, out, channels);
+    hipLaunchKernelGGL((k_conv_mx_prep<AZ_CONV_SPLIT3>), dim3(grid), dim3(256), 0, s, w9, out, channels, nullptr);
   else if (mode == AZ_CONV_FP16)
-    hipLaunchKernelGGL(k_conv_mx_prep<AZ_CONV_FP16>, dim3(grid), dim3(256), 0, s, w9, out, channels);
-  else
+    hipLaunchKernelGGL((k_conv_mx_prep<AZ_CONV_FP16>), dim3(grid), dim3(256), 0, s, w9, out, channels, nullptr);
+  else if (mode == AZ_CONV_FP16X2) {
+    unsigned* hdr = reinterpret_cast<unsigned*>(out + (size_t)9 * channels * channels * 2);
+    AZ_HIP(hipMemsetAsync(hdr, 0, 16, s));
+    hipLaunchKernelGGL((k_conv_mx_prep<AZ_CONV_FP16X2, true>), dim3(grid), dim3(256), 0, s, w9, out, channels, hdr);
+    hipLaunchKernelGGL((k_conv_mx_prep<AZ_CONV_FP16X2>), dim3(grid), dim3(256), 0, s, w9, out, channels, hdr);
+  } else
     return azc::set_error(AZ_ERR_ARG, "az_conv3x3_mx_prep_gpu: unknown mode %d", mode);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
@@ -475,11 +582,18 @@ int launch_mx_cfg(const float* x, const void* wq, const float* bias, const float
   if (channels == 64 && mode == AZ_CONV_SPLIT3) AZ_MX_L(64, AZ_CONV_SPLIT3)
   if (channels == 128 && mode == AZ_CONV_FP16) AZ_MX_L(128, AZ_CONV_FP16)
   if (channels == 64 && mode == AZ_CONV_FP16) AZ_MX_L(64, AZ_CONV_FP16)
+  if (channels == 128 && mode == AZ_CONV_FP16X2) AZ_MX_L(128, AZ_CONV_FP16X2)
+  if (channels == 64 && mode == AZ_CONV_FP16X2) AZ_MX_L(64, AZ_CONV_FP16X2)
 #undef AZ_MX_L
   return azc::set_error(AZ_ERR_ARG, "az_conv3x3_mx_gpu: channels %d / mode %d unsupported",
                         channels, mode);
 }
 }  // namespace
+
+extern "C" int64_t az_conv3x3_mx_prep_bytes(int32_t channels, int32_t mode) {
+  const int planes = mode == AZ_CONV_SPLIT3 ? 3 : (mode == AZ_CONV_FP16X2 ? 2 : 1);
+  return (int64_t)9 * channels * channels * planes * 2 + (mode == AZ_CONV_FP16X2 ? 16 : 0);
+}
 
 extern "C" int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias,
                                  const float* res, float* y, int32_t n_boards,

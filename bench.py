@@ -469,11 +469,23 @@ def trunk_roofline(sp, device, n_boards):
     per_eval = (2 * 64 * C * 9 + 2 * 64 * C * C * 9 * n_convs + 2 * 64 * C * 3
                 + 2 * 128 * 65 + 2 * 64 * 256 + 2 * 256)
     algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
-    traffic = None  # HBM bytes per launch, PMC (scripts/gpu_calls_r05.sh c23), at B = 1,024
+    # HBM bytes per launch from the committed PMC summary (scripts/trunk_traffic.py), used only
+    # for the build it was measured on: the file records the library's source hash, and a
+    # kernel change makes the figure stale (reported as such, traffic null)
+    traffic, source = None, None
     tj = os.path.join(ROOT, "profiles", "trunk_traffic.json")
     if n_boards == 1024 and prec == "fp16x2" and os.path.exists(tj):
         try:
-            traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
+            import az_native as nat
+
+            tjd = json.load(open(tj))
+            current = nat.build_id()
+            source = {"file": "profiles/trunk_traffic.json", "measured": tjd.get("source"),
+                      "build_id": tjd.get("build_id"), "current_build_id": current}
+            if tjd.get("build_id") == current:
+                traffic = tjd.get("hbm_bytes_per_launch")
+            else:
+                source["stale"] = "measured on another build of the library: not reported"
         except (OSError, ValueError):
             traffic = None
     fn = "az_trunk_wino4_heads_gpu" if prec == "fp16x2" else "az_trunk_wino4_heads_fp16_gpu"
@@ -484,6 +496,7 @@ def trunk_roofline(sp, device, n_boards):
             "launches_per_evaluation": -(-n_boards // cap),
             "bound": "mfma", "achieved": round(algorithmic, 1), "peak": MFMA16_PEAK,
             "unit": "TFLOP/s", "frac": round(algorithmic / MFMA16_PEAK, 4), "traffic": traffic,
+            "traffic_source": source,
             "achieved_basis": "algorithmic: the net's %.1f MFLOP per evaluation x boards / launch "
                               "time" % (per_eval / 1e6),
             "mfma_executed_tflops": round(executed, 1),
@@ -842,6 +855,17 @@ def main():
     dt = time.perf_counter() - t0
     prof.pause()
     c1 = sp.counters()
+    # AZ_BENCH_REPEAT=k (diagnostics): k more windows of the same length after the timed one,
+    # timed the same way, reported beside the line (never part of value)
+    repeat = []
+    for _ in range(int(os.environ.get("AZ_BENCH_REPEAT", "0"))):
+        barrier()
+        sp.counters()
+        tr = time.perf_counter()
+        sp.step(a.steps)
+        sp.counters()
+        barrier()
+        repeat.append(round((time.perf_counter() - tr) * 1000.0 / a.steps, 4))
     moves = c1["moves"] - c0["moves"]
     games_done = c1["games_finished"] - c0["games_finished"]
     sims = c1["simulations"] - c0["simulations"]
@@ -891,6 +915,8 @@ def main():
                    "arena_overflows": int(c1["arena_overflows"]),
                    "samples_dropped": int(c1["samples_dropped"])},
     }
+    if repeat:
+        result["detail"]["repeat_ms_per_step"] = repeat
     if dist is not None:
         # what the process group actually was, and every rank's share (a SCALE line shows
         # by itself that N ranks ran and how value was formed)

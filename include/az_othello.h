@@ -338,13 +338,22 @@ int az_conv3x3_cfg_gpu(const float* x, const float* w9, const float* bias, const
  *   AZ_CONV_SPLIT3 — fp32-accurate: each fp32 operand split into three bf16 words, the six
  *                    leading partial products accumulated in fp32 (error at fp32's own
  *                    rounding unit; tests/test_nn_gpu.py measures it against fp64);
- *   AZ_CONV_FP16   — one fp16 product (BASELINE configs[4], fp16 inference).
+ *   AZ_CONV_FP16   — one fp16 product (BASELINE configs[4], fp16 inference);
+ *   AZ_CONV_FP16X2 — fp32-accurate with half of SPLIT3's products: both operands as an fp16
+ *                    pair hi + lo after exact power-of-two scaling (the weights per layer,
+ *                    from the prep's header; the inputs per board, from the board's max |x|
+ *                    reduced inside the kernel), three products accumulated in fp32, the
+ *                    scales removed exactly in the epilogue (FastOthelloNet's 64-channel
+ *                    convs, configs[1]).
  * wq: the weights re-laid by az_conv3x3_mx_prep_gpu from w9 [9][Co][Ci] fp32 into
- * [9][Ci/16][planes][Co][16] 16-bit words (planes = 3 for SPLIT3, 1 for FP16; 16-byte
- * aligned, 9*C*C*planes*2 bytes).  Replaces the same reference layers as az_conv3x3_gpu. */
+ * [9][Ci/16][planes][Co][16] 16-bit words (planes = 3 for SPLIT3, 1 for FP16, 2 for FP16X2;
+ * 16-byte aligned, az_conv3x3_mx_prep_bytes: 9*C*C*planes*2 bytes plus, for FP16X2, a
+ * 16-byte scale header after the words).  Replaces the same reference layers as
+ * az_conv3x3_gpu. */
 enum { AZ_CONV_SPLIT3 = 0, AZ_CONV_FP16 = 1, AZ_CONV_FP16X2 = 2 };
 int az_conv3x3_mx_prep_gpu(const float* w9, void* wq, int32_t channels, int32_t mode,
                            void* stream);
+int64_t az_conv3x3_mx_prep_bytes(int32_t channels, int32_t mode);
 int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias, const float* res,
                       float* y, int32_t n_boards, int32_t channels, int32_t relu, int32_t mode,
                       void* stream);

@@ -13,7 +13,7 @@ import az_build  # noqa: E402
 
 
 def build(name, extra):
-    out = os.path.join(ROOT, "expbuild", name)
+    out = os.path.join(ROOT, os.environ.get("EXP_OUT", "expbuild"), name)  # exp6/: travels
     os.makedirs(out, exist_ok=True)
     want = az_build.source_hash()
     flags = [f for f in az_build.FLAGS if f != "-shared"] + extra.split()

@@ -58,17 +58,23 @@ def main():
     net = AlphaZeroNet(8, 65, 5, 128).eval()
     ps = (AlphaZeroNet, {"board_size": 8, "action_size": 65, "n_res_blocks": 5,
                          "channels": 128}, net.state_dict())
+    # train.py hands every task its whole args dict, num_self_play / num_workers included
+    # (train.py:207-217, 413-420); one_self_play sizes its per-worker batch from them
     args = {"c_puct": 2.0, "num_simulations": sims, "dirichlet_alpha": 1.0,
             "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
-            "lambda": 0.98}
+            "lambda": 0.98, "num_self_play": games, "num_workers": workers}
     ctx = get_context("spawn")
     with ctx.Pool(workers, initializer=_init) as pool:
         pool.map(_play, [(8, dict(args, num_simulations=8), ps, None)] * workers)  # all warm
         t0 = time.perf_counter()
-        plies = sum(pool.imap_unordered(_play, [(8, args, ps, None)] * games, chunksize=1))
+        lens = list(pool.imap_unordered(_play, [(8, args, ps, None)] * games, chunksize=1))
         dt = time.perf_counter() - t0
+    plies = sum(lens)
     print(json.dumps({"workers": workers, "games": games, "sims": sims,
                       "games_per_s": round(games / dt, 4), "plies": plies,
+                      "mean_plies_returned": round(plies / games, 2),
+                      "batch_per_worker": min(int(os.environ.get("AZ_DROPIN_BATCH", "32")),
+                                              -(-games // workers)),
                       "window_s": round(dt, 2),
                       "net": "AlphaZeroNet(5,128) random init, fused HIP inference copy",
                       "path": "train.py Pool -> one_self_play (AZ_DROPIN_BATCH games per worker "

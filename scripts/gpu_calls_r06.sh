@@ -34,4 +34,63 @@ c1() {
   exit 0
 }
 
+
+
+c2() {
+  # bench.py's 20-step two-pipeline window with and without the kernel roofline part before
+  # the warmup (alternating), and the probe's timeline with the kernel part
+  export OUT=gpurun_out/r06b
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run bench20_k_$i 300 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
+    run bench20_nok_$i 300 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel || exit $?
+  done
+  run probe_p2_kb 300 env PROBE_KB=1 python -u scripts/window_probe.py 2 20 20 20 20 20 || exit $?
+  exit 0
+}
+
+c3() {
+  # FastOthelloNet's 64-channel convs in FP16X2 on the direct kernel: accuracy / bit-identity
+  # tests, the reference-net goldens, the drop-in batch order; configs[1] A/B against split3
+  export OUT=gpurun_out/r06c
+  mkdir -p $OUT
+  pyt pytest_fp16x2 600 tests/test_nn_gpu.py -k "direct_fp16x2 or stem_fusion" || exit $?
+  pyt pytest_fast 600 tests/test_net_golden_gpu.py tests/test_pipelined_gpu.py tests/test_engine_gpu.py \
+    -k "fast or drop_in" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_split3 300 env AZ_CONV64_SPLIT3=1 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
+
+c4() {
+  # configs[4]'s fp16 trunk and configs[2]'s fp16x2 trunk as four-board workgroups (exp6/tb4:
+  # -DAZ_W4_TRUNK_BOARDS=4) against the two-board default; train.py's unchanged pool at the
+  # reference's num_self_play = 300 over the job's CPUs
+  export OUT=gpurun_out/r06d
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_c5 300 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+    run bench_c5_tb4 300 env AZ_LIB_PATH=exp6/tb4/libaz_othello.so python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+  done
+  run pool300 600 python scripts/dropin_pool_bench.py 15 300 400 || exit $?
+  exit 0
+}
+
+c5() {
+  # is a slow 20-step window the process or the first window after the warmup?  bench.py's
+  # window followed by six more of the same length in the same process (AZ_BENCH_REPEAT)
+  export OUT=gpurun_out/r06e
+  mkdir -p $OUT
+  for i in 1 2 3 4; do
+    run bench20_rep_$i 300 env AZ_BENCH_REPEAT=6 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel || exit $?
+  done
+  run bench20_rep_p1 300 env AZ_BENCH_REPEAT=6 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel --pipelines 1 || exit $?
+  exit 0
+}
 "$@"

@@ -89,6 +89,10 @@ def main():
     ns = [int(x) for x in sys.argv[2:]] or [20, 20, 20, 8000, 20, 20, 16, 24, 40]
     spg = int(os.environ.get("PROBE_SPG", "8"))
     sp, stagger = build(P, spg=spg)
+    if os.environ.get("PROBE_KB") == "1":  # bench.py's kernel roofline first, as bench.py runs it
+        kb = bench.StepKernelBench(1 << 24, torch.device("cuda", 0))
+        print(json.dumps({"k_step_ms": round(kb.time_ms(), 4), "io_ms": round(kb.time_io_ms(), 4)}),
+              flush=True)
     t = time.perf_counter()
     sp.step(stagger)
     torch.cuda.synchronize()

@@ -136,8 +136,8 @@ def test_inference_copy_fp16x2_small_batches(B):
 def _mx_conv(x, w, b, r, relu, mode):
     C = x.shape[1]
     w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
-    planes = 3 if mode == nat.AZ_CONV_SPLIT3 else 1
-    wq = torch.empty(9 * C * C * planes, dtype=torch.int16, device="cuda")
+    wq = torch.empty(nat.lib.az_conv3x3_mx_prep_bytes(C, mode) // 2, dtype=torch.int16,
+                     device="cuda")
     nat.check(nat.lib.az_conv3x3_mx_prep_gpu(nat.ptr(w9), nat.ptr(wq), C, mode, nat.stream_ptr()),
               "az_conv3x3_mx_prep_gpu")
     y = torch.empty_like(x, memory_format=torch.channels_last)
@@ -208,6 +208,41 @@ def test_conv3x3_split3_is_fp32_accurate(C, B, res, relu):
     assert e_mx.max() <= 2 * e_32.max() + 1e-6, (e_mx.max(), e_32.max())
     assert e_mx.mean() <= 2 * e_32.mean() + 1e-8, (e_mx.mean(), e_32.mean())
     torch.testing.assert_close(y, ref.float().cuda(), **TOL)
+
+
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("B", [1, 3, 130])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_conv3x3_direct_fp16x2_is_fp32_accurate(C, B, res, relu):
+    """The direct kernel's FP16X2 mode (csrc/conv16.hip: fp16 hi + lo operand pairs after
+    exact power-of-two scaling -- the weights per layer, each board by the max |x| its
+    workgroup stages -- three products; FastOthelloNet's 64-channel convs) against fp64: the
+    fp32-accuracy bar of the split3 kernels (max |err| <= 2x the fp32 MFMA kernel's + 1e-6,
+    mean <= 2x), boards from 1e-3 to 1e3 in one batch."""
+    x, w, b, r, ref64 = _case(C, B, C * 29 + B)
+    if B > 1:  # per-board ranges from 1e-3 to 1e3
+        s = torch.logspace(-3, 3, B, device="cuda").view(B, 1, 1, 1)
+        x = (x * s).contiguous(memory_format=torch.channels_last)
+        ref64 = F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), padding=1)
+    rr = r if res else None
+    y = _mx_conv(x, w, b, rr, relu, nat.AZ_CONV_FP16X2)
+    w9 = w.permute(2, 3, 0, 1).reshape(9, C, C).contiguous()
+    y32 = torch.empty_like(x, memory_format=torch.channels_last)
+    nat.check(nat.lib.az_conv3x3_gpu(nat.ptr(x), nat.ptr(w9), nat.ptr(b), None if rr is None else nat.ptr(rr),
+                                     nat.ptr(y32), B, C, int(relu), nat.stream_ptr()), "az_conv3x3_gpu")
+    torch.cuda.synchronize()
+    ref = ref64 + (r.cpu().double() if res else 0)
+    if relu:
+        ref = F.relu(ref)
+    e_h = (y.cpu().double() - ref).abs()
+    e_32 = (y32.cpu().double() - ref).abs()
+    assert torch.isfinite(y).all()
+    assert e_h.max() <= 2 * e_32.max() + 1e-6, (e_h.max(), e_32.max())
+    assert e_h.mean() <= 2 * e_32.mean() + 1e-8, (e_h.mean(), e_32.mean())
+    # per board too (the global bar is set by the 1e3 boards): a board scaled by another
+    # board's range would lose the lo words of its small values -- ~1e-5 on a 1e-3 board
+    for bi in range(B):
+        assert e_h[bi].max() <= 4 * e_32[bi].max() + 1e-7, (bi, e_h[bi].max(), e_32[bi].max())
 
 
 @pytest.mark.parametrize("C", [64, 128])
@@ -385,7 +420,7 @@ def test_inference_copy_fp16_trunk(kind):
 
 
 @pytest.mark.parametrize("kind", ["az", "fast"])
-@pytest.mark.parametrize("precision", ["split3", "fp16"])
+@pytest.mark.parametrize("precision", ["split3", "fp16", "fp16x2"])
 def test_stem_fusion_is_bit_identical(kind, precision):
     """The stem evaluated inside the first block's convs (az_conv3x3_mx_stem_gpu) gives the
     same trunk output bit for bit as the stem kernel + plain convs."""
