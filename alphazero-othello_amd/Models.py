@@ -853,7 +853,25 @@ class FusedInferenceNet(nn.Module, Inference):
                         "bias": bias, "ld": ld,
                         "w2": v2.weight.detach().float().reshape(-1).contiguous(),
                         "b2": v2.bias.detach().float().contiguous()}
+            if self.fast_gemm and C == 64:
+                # az_heads_fast_gemm_gpu's operands: columns 0..127 scaled by 2^wshift (max
+                # |W| < 2^(15 - wshift)) and split into fp16 hi / lo planes laid out as the MFMA
+                # B fragments [K/16][hi, lo][128][16]; column 128 stays fp32 (its FMAs)
+                w128 = wt[:, :128]
+                e = int(torch.frexp(w128.abs().max())[1].item())  # max |W| < 2^e
+                ws = w128 * (2.0 ** (15 - e))  # exact: a power of two
+                hi = ws.half()
+                lo = (ws - hi.float()).half()
+                planes = torch.stack([p.view(64 * C // 16, 16, 128).permute(0, 2, 1)
+                                      for p in (hi, lo)], 1).contiguous()  # [K/16][2][128][16]
+                self._fw.update(gq=planes.view(torch.int16), g128=wt[:, 128].contiguous(),
+                                gshift=15 - e, gS=self.fast_gemm_splits)
         return True
+
+    # AZ_FAST_GEMM (default on): the heads GEMM on az_heads_fast_gemm_gpu (fp16x2 MFMA, split
+    # over AZ_FAST_GEMM_SPLITS = 8 slices of the 4,096 features) instead of torch.bmm (fp32)
+    fast_gemm = os.environ.get("AZ_FAST_GEMM", "1") == "1"
+    fast_gemm_splits = int(os.environ.get("AZ_FAST_GEMM_SPLITS", "8"))
 
     def evaluate_into(self, planes, priors, values, stem_done=False):
         """Leaf evaluation straight into the engine's buffers: priors float32 [B, 65]
@@ -869,8 +887,15 @@ class FusedInferenceNet(nn.Module, Inference):
             fw = self._fw
             t = self.tail(self._trunk(planes.view(B, 1, 8, 8)))
             hf = t.permute(0, 2, 3, 1).reshape(B, -1)  # a view of the channels-last output
-            S = fw["S"]
-            part = torch.bmm(hf.view(B, S, -1).transpose(0, 1), fw["wk"])  # [S, B, ld]
+            if "gq" in fw:
+                S = fw["gS"]
+                part = torch.empty(S, B, fw["ld"], dtype=torch.float32, device=hf.device)
+                nat.check(nat.lib.az_heads_fast_gemm_gpu(
+                    nat.ptr(hf), nat.ptr(fw["gq"]), nat.ptr(fw["g128"]), fw["gshift"],
+                    nat.ptr(part), fw["ld"], S, B, nat.stream_ptr()), "az_heads_fast_gemm_gpu")
+            else:
+                S = fw["S"]
+                part = torch.bmm(hf.view(B, S, -1).transpose(0, 1), fw["wk"])  # [S, B, ld]
             nat.check(nat.lib.az_heads_fast_finish_gpu(
                 nat.ptr(part), fw["ld"], S, nat.ptr(fw["bias"]), nat.ptr(fw["w2"]),
                 nat.ptr(fw["b2"]), nat.ptr(priors), nat.ptr(values), B, nat.stream_ptr()),

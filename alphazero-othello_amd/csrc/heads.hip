@@ -133,3 +133,179 @@ extern "C" int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }
+
+// FastOthelloNet's heads GEMM (the host's torch.bmm before az_heads_fast_finish_gpu) on the
+// 16-bit MFMA pipe, fp32-accurate: logits partials part[s][b][0..128] = sum over the s-th
+// slice of the K = 4,096 flattened tail features (NHWC order, the permuted FC weights' rows)
+// of x[b][k] * W[k][n], for n = [fc_policy; fc_value1] (129 columns).
+//   * Workgroup = 32 boards (one MFMA row tile) x one K slice of 4,096 / S; four waves, wave w
+//     the columns 32w .. 32w+31 (v_mfma_f32_32x32x16_f16).
+//   * FP16X2 numerics as the trunk's: the weights scaled once by 2^wshift (the host prepares
+//     wq = [K/16][hi, lo][128][16] fp16 words), each board's slice scaled by 2^(15 - e) with
+//     max |x| < 2^e over the slice (reduced in the workgroup while the slice is staged), three
+//     products lo*hi + hi*lo + hi*hi accumulated in fp32, both scales removed exactly in the
+//     epilogue.  A partial's scale is its own slice's: the partials are unscaled fp32 sums,
+//     which the finish kernel adds in slice order as before.
+//   * Column 128 (fc_value1's last unit, the one column past four MFMA tiles) as fp32 FMAs
+//     on the staged slice, reduced in a fixed order (deterministic).
+namespace {
+template <int S>
+struct HG {
+  static constexpr int K = 4096, KS = K / S, STEPS = KS / 16, ITER = KS / 32;
+  static constexpr int SLAB = 1040;  // one (step, plane): 32 rows x 32 B, + 16 B (write banks)
+  static constexpr int LDS_BYTES = STEPS * 2 * SLAB;
+  static constexpr int PD = 3;       // weight fragments requested this many steps ahead
+  static_assert(STEPS % 4 == 0 && ITER >= 1, "slice");
+};
+
+typedef _Float16 hf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hf16x4 __attribute__((ext_vector_type(4)));
+typedef float hf32x16 __attribute__((ext_vector_type(16)));
+typedef float hf32x4 __attribute__((ext_vector_type(4)));
+
+template <int S>
+__global__ __launch_bounds__(256) void k_heads_fast_gemm(const float* __restrict__ x,
+                                                         const char* __restrict__ wq,
+                                                         const float* __restrict__ w128,
+                                                         int wshift, float* __restrict__ part,
+                                                         int ld, int n_boards) {
+  using G = HG<S>;
+  extern __shared__ float4 lds4[];
+  char* lds = reinterpret_cast<char*>(lds4);
+  __shared__ unsigned s_max[32];
+  __shared__ float s_c[G::ITER][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int b0 = blockIdx.x * 32, sl = blockIdx.y, k0 = sl * G::KS;
+  if (tid < 32) s_max[tid] = 0u;
+
+  // the wave's first weight fragments in flight while the slice is staged
+  const int wlane = (32 * wave + r) * 32 + h * 16;
+  auto load_b = [&](hf16x8 (&f)[2], int j) {
+    const char* p = wq + (size_t)(k0 / 16 + j) * 2 * 128 * 32 + wlane;
+    f[0] = *reinterpret_cast<const hf16x8*>(p);
+    f[1] = *reinterpret_cast<const hf16x8*>(p + 128 * 32);
+  };
+  hf16x8 bf[4][2];
+#pragma unroll
+  for (int j = 0; j < G::PD; ++j) load_b(bf[j], j);
+
+  // ---- the slice: element (row, k4) of iteration i = i * 256 + tid (rows are wave-uniform)
+  constexpr int Q = G::KS / 4;  // float4s per row
+  float4 a[G::ITER];
+  float4 wv[G::ITER];
+#pragma unroll
+  for (int i = 0; i < G::ITER; ++i) {
+    const int idx = i * 256 + tid, row = idx / Q, k4 = idx % Q, b = b0 + row;
+    a[i] = b < n_boards ? reinterpret_cast<const float4*>(x + (size_t)b * G::K + k0)[k4]
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    wv[i] = reinterpret_cast<const float4*>(w128 + k0)[k4];
+  }
+  __syncthreads();  // s_max initialised
+#pragma unroll
+  for (int i = 0; i < G::ITER; ++i) {
+    const int row = (i * 256 + wave * 64) / Q;
+    unsigned m = max(max(__float_as_uint(fabsf(a[i].x)), __float_as_uint(fabsf(a[i].y))),
+                     max(__float_as_uint(fabsf(a[i].z)), __float_as_uint(fabsf(a[i].w))));
+    float c = fmaf(a[i].w, wv[i].w, fmaf(a[i].z, wv[i].z, fmaf(a[i].y, wv[i].y, a[i].x * wv[i].x)));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+      c += __shfl_xor(c, off, 64);
+    }
+    if (lane == 0) {
+      atomicMax(&s_max[row], m);
+      s_c[i][wave] = c;
+    }
+  }
+  __syncthreads();
+  // split into the LDS image [step][plane][row][16] (fp16 hi, lo of x * 2^(15 - e_row))
+#pragma unroll
+  for (int i = 0; i < G::ITER; ++i) {
+    const int idx = i * 256 + tid, row = idx / Q, kl = (idx % Q) * 4;
+    const unsigned mb = s_max[row];
+    const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;  // max < 2^e
+    const float sc = ldexpf(1.0f, 15 - e);
+    const hf32x4 v = {a[i].x * sc, a[i].y * sc, a[i].z * sc, a[i].w * sc};  // exact
+    const hf16x4 hi = __builtin_convertvector(v, hf16x4);
+    const hf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, hf32x4), hf16x4);
+    char* dst = lds + ((kl >> 4) * 2) * G::SLAB + row * 32 + (kl & 15) * 2;
+    *reinterpret_cast<hf16x4*>(dst) = hi;
+    *reinterpret_cast<hf16x4*>(dst + G::SLAB) = lo;
+  }
+  __syncthreads();
+
+  // ---- K loop: per step, A fragments (all 32 rows) from LDS, B from the weight ring
+  hf32x16 acc = {};
+  const int aoff = r * 32 + h * 16;
+#pragma unroll 4
+  for (int j = 0; j < G::STEPS; ++j) {
+    const char* ap = lds + (j * 2) * G::SLAB + aoff;
+    const hf16x8 ahi = *reinterpret_cast<const hf16x8*>(ap);
+    const hf16x8 alo = *reinterpret_cast<const hf16x8*>(ap + G::SLAB);
+    const int jn = j + G::PD < G::STEPS ? j + G::PD : G::STEPS - 1;
+    load_b(bf[(j + G::PD) & 3], jn);
+    const hf16x8(&b)[2] = bf[j & 3];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b[0], acc, 0, 0, 0);
+  }
+
+  // ---- epilogue: D[row][col], col = lane & 31, row = (k & 3) + 8 (k >> 2) + 4 h
+  float* out = part + (size_t)sl * n_boards * ld;
+  const int col = 32 * wave + r;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int row = (k & 3) + 8 * (k >> 2) + 4 * h, b = b0 + row;
+    const unsigned mb = s_max[row];
+    const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;
+    if (b < n_boards) out[(size_t)b * ld + col] = acc[k] * ldexpf(1.0f, -(15 - e) - wshift);
+  }
+  if (tid < 32 && b0 + tid < n_boards) {
+    float c = 0.0f;  // column 128: this row's wave partials in (iteration, wave) order
+#pragma unroll
+    for (int i = 0; i < G::ITER; ++i)
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        if ((i * 256 + w * 64) / Q == tid) c += s_c[i][w];
+    float* o = out + (size_t)(b0 + tid) * ld;
+    o[128] = c;
+    for (int n = 129; n < ld; ++n) o[n] = 0.0f;
+  }
+}
+
+template <int S>
+int launch_heads_fast_gemm(const float* x, const void* wq, const float* w128, int wshift,
+                           float* part, int ld, int n_boards, hipStream_t s) {
+  using G = HG<S>;
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in once
+  if (!attr_set) {
+    AZ_HIP(hipFuncSetAttribute((const void*)k_heads_fast_gemm<S>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES));
+    attr_set = true;
+  }
+  const dim3 grid((unsigned)((n_boards + 31) / 32), S);
+  hipLaunchKernelGGL((k_heads_fast_gemm<S>), grid, dim3(256), G::LDS_BYTES, s, x,
+                     static_cast<const char*>(wq), w128, wshift, part, ld, n_boards);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
+}
+}  // namespace
+
+extern "C" int az_heads_fast_gemm_gpu(const float* x, const void* wq, const float* w128,
+                                      int32_t wshift, float* part, int32_t ld, int32_t splits,
+                                      int32_t n_boards, void* stream) {
+  AZ_REQUIRE(n_boards >= 0 && ld >= 129, AZ_ERR_ARG,
+             "az_heads_fast_gemm_gpu: n_boards %d < 0 or ld %d < 129", n_boards, ld);
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(x && wq && w128 && part, AZ_ERR_ARG, "az_heads_fast_gemm_gpu: null buffer");
+  AZ_REQUIRE(((uintptr_t)x | (uintptr_t)wq | (uintptr_t)w128) % 16 == 0, AZ_ERR_ARG,
+             "az_heads_fast_gemm_gpu: buffers must be 16-byte aligned");
+  AZ_REQUIRE(wshift > -126 && wshift < 126, AZ_ERR_ARG, "az_heads_fast_gemm_gpu: wshift %d",
+             wshift);
+  hipStream_t s = azc::as_stream(stream);
+  if (splits == 4) return launch_heads_fast_gemm<4>(x, wq, w128, wshift, part, ld, n_boards, s);
+  if (splits == 8) return launch_heads_fast_gemm<8>(x, wq, w128, wshift, part, ld, n_boards, s);
+  return azc::set_error(AZ_ERR_ARG, "az_heads_fast_gemm_gpu: splits must be 4 or 8, got %d",
+                        splits);
+}

@@ -84,6 +84,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=24000,
                     help="untimed steps; the default (about one game length at 400 sims) lets "
                          "the first games finish so plies/game is measured in this run")
+    ap.add_argument("--settle", type=int, default=3,
+                    help="untimed windows of --steps steps, each bracketed like the timed one, "
+                         "between the warmup and the timed window (the post-load power "
+                         "transient: profiles/r06_window_power.json)")
+    ap.add_argument("--sustained-steps", type=int, default=2000,
+                    help="the warmup's last block of this many steps, timed on its own and "
+                         "reported as detail.sustained_ms_per_step (0 = off)")
     ap.add_argument("--warmup-exact", action="store_true",
                     help="run exactly --warmup untimed steps, not the steady-state minimum "
                          "(short profiler runs; the value is then not steady state)")
@@ -837,6 +844,30 @@ def main():
         ms_io_kernel = kb.time_io_ms()
     sp.step(warmup_run)
     barrier()
+    # the sustained rate (reported beside the line, never part of value): the untimed warmup's
+    # continuation, --sustained-steps more steps in one block
+    sustained = None
+    if a.sustained_steps > 0:
+        ts = time.perf_counter()
+        sp.step(a.sustained_steps)
+        barrier()
+        sustained = (time.perf_counter() - ts) * 1000.0 / a.sustained_steps
+    # settle windows (untimed): --settle blocks of exactly the timed window's shape (barrier,
+    # counters, --steps steps, counters, barrier).  After seconds of sustained full load the
+    # chip's power management makes the next one or two short windows up to ~25 % slower than
+    # both the sustained rate and every later window (profiles/r06_window_power.json: a
+    # window's time also grows with the idle pause before it); these blocks let that transient
+    # pass before the timed window, which then sees the conditions every later window does
+    settle = []
+    for _ in range(a.settle):
+        barrier()
+        sp.counters()
+        tq = time.perf_counter()
+        sp.step(a.steps)
+        sp.counters()
+        barrier()
+        settle.append(round((time.perf_counter() - tq) * 1000.0 / a.steps, 4))
+    barrier()
     prof = _ProfilerWindow()  # AZ_PROF_WINDOW=1: rocprofv3 --selected-regions traces the window only
     c0 = sp.counters()
     t0 = time.perf_counter()
@@ -883,7 +914,7 @@ def main():
     result = {
         "metric": f"self-play games/sec (whole node), 8x8 Othello @ {a.sims} MCTS sims/move",
         "value": round(float(value), 4), "unit": "games/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "warmup_steps_run": warmup_run,
+        "steps": a.steps, "warmup": a.warmup, "warmup_steps_run": warmup_run + max(0, a.sustained_steps) + a.settle * a.steps,
         "ms_per_step": round(t_max * 1000.0 / a.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": DTYPE_LABEL[a.conv_precision],
         "data": "synthetic: self-play from the initial position, random-init net weights",
@@ -917,6 +948,11 @@ def main():
     }
     if repeat:
         result["detail"]["repeat_ms_per_step"] = repeat
+    if settle:
+        result["detail"]["settle_ms_per_step"] = settle
+    if sustained is not None:
+        result["detail"]["sustained_ms_per_step"] = round(sustained, 4)
+        result["detail"]["sustained_steps"] = a.sustained_steps
     if dist is not None:
         # what the process group actually was, and every rank's share (a SCALE line shows
         # by itself that N ranks ran and how value was formed)

@@ -93,4 +93,40 @@ c5() {
   run bench20_rep_p1 300 env AZ_BENCH_REPEAT=6 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel --pipelines 1 || exit $?
   exit 0
 }
+
+c6() {
+  # FastOthelloNet's heads GEMM on az_heads_fast_gemm_gpu (fp16x2 MFMA) against torch.bmm;
+  # the short window after sustained load with idle pauses (power management?)
+  export OUT=gpurun_out/r06f
+  mkdir -p $OUT
+  pyt pytest_gemm 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py tests/test_pipelined_gpu.py \
+    -k "heads_fast_gemm or fast" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_bmm 300 env AZ_FAST_GEMM=0 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  run power_p2 400 python -u scripts/window_power.py 2 || exit $?
+  run power_p1 400 python -u scripts/window_power.py 1 || exit $?
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
+
+c7() {
+  # bench.py with the settle windows (default 3) and the sustained block: two pipelines x3,
+  # one pipeline x2, and the 8000-step window on the same box
+  export OUT=gpurun_out/r06g
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run bench20_p2_$i 300 env AZ_BENCH_REPEAT=3 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel || exit $?
+  done
+  for i in 1 2; do
+    run bench20_p1_$i 300 env AZ_BENCH_REPEAT=3 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel --pipelines 1 || exit $?
+  done
+  run bench8000_p2 300 python bench.py --gpus 1 --steps 8000 --warmup 5 --skip-cpu --skip-kernel --settle 0 || exit $?
+  run bench8000_p1 300 python bench.py --gpus 1 --steps 8000 --warmup 5 --skip-cpu --skip-kernel --settle 0 --pipelines 1 || exit $?
+  exit 0
+}
 "$@"

@@ -582,3 +582,43 @@ def test_trunk_heads_bit_identical(B, monkeypatch):
         pr, va = out[name]
         assert torch.equal(pr, out["separate"][0].expand_as(pr)), name
         assert torch.equal(va, out["separate"][1].expand_as(va)), name
+
+
+@pytest.mark.parametrize("B", [1, 33, 2048])
+@pytest.mark.parametrize("splits", [4, 8])
+def test_heads_fast_gemm_is_fp32_accurate(B, splits):
+    """az_heads_fast_gemm_gpu (FastOthelloNet's heads GEMM on the 16-bit MFMA pipe, fp16 hi /
+    lo operands after power-of-two scaling -- per board and slice for the features, per
+    matrix for the weights -- three products, column 128 as fp32 FMAs) against fp64: the
+    summed partials within 2x torch's fp32 GEMM error (+ 1e-6), per board too (boards from
+    1e-3 to 1e3), columns past 128 zero, a ragged last row tile."""
+    from Models import FusedInferenceNet
+
+    g = torch.Generator().manual_seed(B * 7 + splits)
+    x = torch.randn(B, 4096, generator=g).relu()
+    if B > 1:
+        x = x * torch.logspace(-3, 3, B).view(B, 1)
+    w = torch.randn(4096, 129, generator=g) / 64.0
+    ref = x.double() @ w.double()
+    xd, wd = x.cuda().contiguous(), w.cuda()
+    e = int(torch.frexp(wd[:, :128].abs().max())[1].item())
+    ws = wd[:, :128] * (2.0 ** (15 - e))
+    hi = ws.half()
+    lo = (ws - hi.float()).half()
+    wq = torch.stack([p.view(256, 16, 128).permute(0, 2, 1) for p in (hi, lo)], 1).contiguous()
+    w128 = wd[:, 128].contiguous()
+    ld = 132
+    part = torch.full((splits, B, ld), float("nan"), device="cuda")
+    nat.check(nat.lib.az_heads_fast_gemm_gpu(nat.ptr(xd), nat.ptr(wq.view(torch.int16)),
+                                             nat.ptr(w128), 15 - e, nat.ptr(part), ld, splits,
+                                             B, nat.stream_ptr()), "az_heads_fast_gemm_gpu")
+    torch.cuda.synchronize()
+    assert torch.isfinite(part).all()
+    assert (part[:, :, 129:] == 0).all()
+    got = part.double().sum(0)[:, :129].cpu()
+    f32 = (xd @ wd).double().cpu()
+    e_g, e_32 = (got - ref).abs(), (f32 - ref).abs()
+    assert e_g.max() <= 2 * e_32.max() + 1e-6, (e_g.max(), e_32.max())
+    for bi in range(B):
+        assert e_g[bi].max() <= 2 * e_32[bi].max() + 1e-7 * (1 + ref[bi].abs().max()), bi
+    assert FusedInferenceNet.fast_gemm_splits in (4, 8)
