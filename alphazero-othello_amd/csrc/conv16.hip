@@ -33,6 +33,8 @@
 //     (tap, 16-channel) steps ahead.  No LDS stage, so the main loop has no barrier.
 //   * A fragments of the next step are read from LDS during this step's MFMAs.
 //   * Epilogue straight from the accumulators: + bias, + residual, ReLU, NHWC store.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -178,15 +180,16 @@ struct StemArgs {
 
 // stem output for 4 channels c..c+3 at square p of the staged plane grid `pl` (10 x 10,
 // zero border): same tap order and fmaf chain as k_conv_stem
-__device__ __forceinline__ float4 stem4(const float* pl, int p, int c, int C, StemArgs st) {
+// (sw / sb: the four channels' weights and bias, loaded once by the caller)
+__device__ __forceinline__ float4 stem4(const float* pl, int p, const float4 (&sw)[9], float4 sb) {
   const int py = p >> 3, px = p & 7;
-  float4 acc = *reinterpret_cast<const float4*>(st.b + c);
+  float4 acc = sb;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
     if ((unsigned)yy < 8u && (unsigned)xx < 8u) {
       const float v = pl[(yy + 1) * 10 + xx + 1];
-      const float4 wv = *reinterpret_cast<const float4*>(st.w + t * C + c);
+      const float4 wv = sw[t];
       acc.x = fmaf(v, wv.x, acc.x);
       acc.y = fmaf(v, wv.y, acc.y);
       acc.z = fmaf(v, wv.z, acc.z);
@@ -245,6 +248,16 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
       __syncthreads();
     }
     const float4* src = reinterpret_cast<const float4*>(x + (size_t)b0 * 64 * C);
+    // STEM = 1: a thread's channel quad is the same in every iteration (kThreads is a multiple
+    // of C / 4), so its stem weights and bias are loaded once
+    static_assert(kThreads % (C / 4) == 0, "one channel quad per thread");
+    float4 stw[9], stb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (STEM == 1) {
+      const int c = (tid % (C / 4)) * 4;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) stw[t] = *reinterpret_cast<const float4*>(st.w + t * C + c);
+      stb = *reinterpret_cast<const float4*>(st.b + c);
+    }
     float4 val[ITER];
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
       if (STEM == 1) {
         if (v < nb * 64 * (C / 4)) {
           const int pos = v / (C / 4);
-          val[i] = stem4(s_plane[pos >> 6], pos & 63, (v % (C / 4)) * 4, C, st);
+          val[i] = stem4(s_plane[pos >> 6], pos & 63, stw, stb);
         }
       } else if (!(AZ_MX_EXP & 4) && v < nb * 64 * (C / 4)) {
         val[i] = src[v];
@@ -595,11 +608,23 @@ extern "C" int64_t az_conv3x3_mx_prep_bytes(int32_t channels, int32_t mode) {
   return (int64_t)9 * channels * channels * planes * 2 + (mode == AZ_CONV_FP16X2 ? 16 : 0);
 }
 
+namespace {
+// the default workgroup shape: 1 board (measured faster at every shape in split3,
+// profiles/r01_conv_mx.jsonl); AZ_MX_CFG=0 (experiments): 2 boards per workgroup
+int mx_default_cfg() {
+  static const int cfg = [] {
+    const char* e = getenv("AZ_MX_CFG");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return cfg;
+}
+}  // namespace
+
 extern "C" int az_conv3x3_mx_gpu(const float* x, const void* wq, const float* bias,
                                  const float* res, float* y, int32_t n_boards,
                                  int32_t channels, int32_t relu, int32_t mode, void* stream) {
-  // 1 board per workgroup measured faster at every shape (profiles/r01_conv_mx.jsonl)
-  return az_conv3x3_mx_cfg_gpu(x, wq, bias, res, y, n_boards, channels, relu, mode, 1, stream);
+  return az_conv3x3_mx_cfg_gpu(x, wq, bias, res, y, n_boards, channels, relu, mode,
+                               mx_default_cfg(), stream);
 }
 
 extern "C" int az_conv3x3_mx_cfg_gpu(const float* x, const void* wq, const float* bias,
@@ -636,5 +661,6 @@ extern "C" int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w,
   // role 1: input = stem(planes), no residual; role 2: residual = stem(planes) (res is a
   // non-null placeholder that selects the residual epilogue; it is not read)
   return launch_mx_cfg(role == 1 ? stem_b : x, wq, bias, role == 2 ? stem_b : nullptr, y,
-                       n_boards, channels, 1, mode, 1, azc::as_stream(stream), st, role);
+                       n_boards, channels, 1, mode, mx_default_cfg(), azc::as_stream(stream), st,
+                       role);
 }
