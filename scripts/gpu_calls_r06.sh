@@ -129,4 +129,24 @@ c7() {
   run bench8000_p1 300 python bench.py --gpus 1 --steps 8000 --warmup 5 --skip-cpu --skip-kernel --settle 0 --pipelines 1 || exit $?
   exit 0
 }
+
+c8() {
+  # conv16 stem weights hoisted (bit-identity and accuracy tests), two-board direct
+  # workgroups (AZ_MX_CFG=0) against one for configs[1]; configs[4] with the four-board trunk
+  # (exp6/tb4); train.py's unchanged pool at num_self_play = 300
+  export OUT=gpurun_out/r06h
+  mkdir -p $OUT
+  pyt pytest_c16 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py \
+    -k "stem_fusion or direct_fp16x2 or split3_is or fast" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_cfg0 300 env AZ_MX_CFG=0 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  for i in 1 2; do
+    run bench_c5 300 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+    run bench_c5_tb4 300 env AZ_LIB_PATH=exp6/tb4/libaz_othello.so python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+  done
+  run pool300 600 python scripts/dropin_pool_bench.py 15 300 400 || exit $?
+  exit 0
+}
 "$@"
