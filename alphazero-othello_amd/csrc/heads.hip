@@ -147,7 +147,7 @@ extern "C" int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t
 //     epilogue.  A partial's scale is its own slice's: the partials are unscaled fp32 sums,
 //     which the finish kernel adds in slice order as before.
 //   * Column 128 (fc_value1's last unit, the one column past four MFMA tiles) as fp32 FMAs
-//     on the staged slice, reduced in a fixed order (deterministic).
+//     on the staged slice: eight lanes per row, reduced in a fixed order (deterministic).
 namespace {
 template <int S>
 struct HG {
@@ -173,11 +173,10 @@ __global__ __launch_bounds__(256) void k_heads_fast_gemm(const float* __restrict
   extern __shared__ float4 lds4[];
   char* lds = reinterpret_cast<char*>(lds4);
   __shared__ unsigned s_max[32];
-  __shared__ float s_c[G::ITER][4];
+  __shared__ float s_c[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int b0 = blockIdx.x * 32, sl = blockIdx.y, k0 = sl * G::KS;
-  if (tid < 32) s_max[tid] = 0u;
 
   // the wave's first weight fragments in flight while the slice is staged
   const int wlane = (32 * wave + r) * 32 + h * 16;
@@ -190,48 +189,53 @@ __global__ __launch_bounds__(256) void k_heads_fast_gemm(const float* __restrict
 #pragma unroll
   for (int j = 0; j < G::PD; ++j) load_b(bf[j], j);
 
-  // ---- the slice: element (row, k4) of iteration i = i * 256 + tid (rows are wave-uniform)
+  // ---- the slice: thread t owns row t / 8 and the float4 columns k4 = t % 8 + 8 i (eight
+  // lanes per row read 128 contiguous bytes per iteration), so a row's max |x| and its
+  // column-128 dot are per-thread sums reduced over eight lanes in a fixed order
   constexpr int Q = G::KS / 4;  // float4s per row
+  static_assert(Q == 8 * G::ITER, "eight lanes per row");
+  const int row = tid >> 3, q0 = tid & 7;
   float4 a[G::ITER];
-  float4 wv[G::ITER];
+  {
+    const bool live = b0 + row < n_boards;
+    const float4* xr = reinterpret_cast<const float4*>(x + (size_t)(live ? b0 + row : 0) * G::K + k0);
+    const float4* wr = reinterpret_cast<const float4*>(w128 + k0);
+    unsigned m = 0u;
+    float c = 0.0f;
 #pragma unroll
-  for (int i = 0; i < G::ITER; ++i) {
-    const int idx = i * 256 + tid, row = idx / Q, k4 = idx % Q, b = b0 + row;
-    a[i] = b < n_boards ? reinterpret_cast<const float4*>(x + (size_t)b * G::K + k0)[k4]
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    wv[i] = reinterpret_cast<const float4*>(w128 + k0)[k4];
-  }
-  __syncthreads();  // s_max initialised
+    for (int i = 0; i < G::ITER; ++i) {
+      a[i] = live ? xr[q0 + 8 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 wv = wr[q0 + 8 * i];
+      m = max(m, max(max(__float_as_uint(fabsf(a[i].x)), __float_as_uint(fabsf(a[i].y))),
+                     max(__float_as_uint(fabsf(a[i].z)), __float_as_uint(fabsf(a[i].w)))));
+      c = fmaf(a[i].w, wv.w, fmaf(a[i].z, wv.z, fmaf(a[i].y, wv.y, fmaf(a[i].x, wv.x, c))));
+    }
 #pragma unroll
-  for (int i = 0; i < G::ITER; ++i) {
-    const int row = (i * 256 + wave * 64) / Q;
-    unsigned m = max(max(__float_as_uint(fabsf(a[i].x)), __float_as_uint(fabsf(a[i].y))),
-                     max(__float_as_uint(fabsf(a[i].z)), __float_as_uint(fabsf(a[i].w))));
-    float c = fmaf(a[i].w, wv[i].w, fmaf(a[i].z, wv[i].z, fmaf(a[i].y, wv[i].y, a[i].x * wv[i].x)));
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
+    for (int off = 4; off > 0; off >>= 1) {  // the row's eight lanes (aligned groups of 8)
       m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
       c += __shfl_xor(c, off, 64);
     }
-    if (lane == 0) {
-      atomicMax(&s_max[row], m);
-      s_c[i][wave] = c;
+    if (q0 == 0) {
+      s_max[row] = m;
+      s_c[row] = c;
     }
   }
   __syncthreads();
   // split into the LDS image [step][plane][row][16] (fp16 hi, lo of x * 2^(15 - e_row))
-#pragma unroll
-  for (int i = 0; i < G::ITER; ++i) {
-    const int idx = i * 256 + tid, row = idx / Q, kl = (idx % Q) * 4;
+  {
     const unsigned mb = s_max[row];
     const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;  // max < 2^e
     const float sc = ldexpf(1.0f, 15 - e);
-    const hf32x4 v = {a[i].x * sc, a[i].y * sc, a[i].z * sc, a[i].w * sc};  // exact
-    const hf16x4 hi = __builtin_convertvector(v, hf16x4);
-    const hf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, hf32x4), hf16x4);
-    char* dst = lds + ((kl >> 4) * 2) * G::SLAB + row * 32 + (kl & 15) * 2;
-    *reinterpret_cast<hf16x4*>(dst) = hi;
-    *reinterpret_cast<hf16x4*>(dst + G::SLAB) = lo;
+#pragma unroll
+    for (int i = 0; i < G::ITER; ++i) {
+      const int kl = (q0 + 8 * i) * 4;
+      const hf32x4 v = {a[i].x * sc, a[i].y * sc, a[i].z * sc, a[i].w * sc};  // exact
+      const hf16x4 hi = __builtin_convertvector(v, hf16x4);
+      const hf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, hf32x4), hf16x4);
+      char* dst = lds + ((kl >> 4) * 2) * G::SLAB + row * 32 + (kl & 15) * 2;
+      *reinterpret_cast<hf16x4*>(dst) = hi;
+      *reinterpret_cast<hf16x4*>(dst + G::SLAB) = lo;
+    }
   }
   __syncthreads();
 
@@ -261,15 +265,9 @@ __global__ __launch_bounds__(256) void k_heads_fast_gemm(const float* __restrict
     const int be = (int)((mb >> 23) & 0xff), e = be == 0 ? 0 : be - 126;
     if (b < n_boards) out[(size_t)b * ld + col] = acc[k] * ldexpf(1.0f, -(15 - e) - wshift);
   }
-  if (tid < 32 && b0 + tid < n_boards) {
-    float c = 0.0f;  // column 128: this row's wave partials in (iteration, wave) order
-#pragma unroll
-    for (int i = 0; i < G::ITER; ++i)
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-        if ((i * 256 + w * 64) / Q == tid) c += s_c[i][w];
+  if (tid < 32 && b0 + tid < n_boards) {  // column 128 (fp32 FMAs), columns past it zero
     float* o = out + (size_t)(b0 + tid) * ld;
-    o[128] = c;
+    o[128] = s_c[tid];
     for (int n = 129; n < ld; ++n) o[n] = 0.0f;
   }
 }
