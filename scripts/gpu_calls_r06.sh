@@ -149,4 +149,19 @@ c8() {
   run pool300 600 python scripts/dropin_pool_bench.py 15 300 400 || exit $?
   exit 0
 }
+
+c9() {
+  # heads GEMM staging by row lane groups (accuracy test, configs[1] bench), configs[1] as
+  # four pipelines, and the default bench line (the driver's command)
+  export OUT=gpurun_out/r06i
+  mkdir -p $OUT
+  pyt pytest_gemm 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py tests/test_pipelined_gpu.py \
+    -k "heads_fast_gemm or fast" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_p4 300 python bench.py --workload c2 --skip-cpu --skip-kernel --pipelines 4 || exit $?
+  done
+  run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+  exit 0
+}
 "$@"
