@@ -164,4 +164,46 @@ c9() {
   run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
   exit 0
 }
+
+f1() {
+  # the whole GPU suite and smoke() on the current tree
+  export OUT=gpurun_out/r06j
+  mkdir -p $OUT
+  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  exit 0
+}
+
+f2() {
+  # the trunk launch's HBM bytes for this build (profiles/trunk_traffic.json keyed on the build
+  # id), then the default bench line (the driver's command) and its rocprofv3 kernel summary
+  export OUT=gpurun_out/r06k
+  mkdir -p $OUT
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    run hbm_$i 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/hbm_$i -o pmc -- \
+      python3 scripts/trunk_heads_one.py 1024 20 || exit $?
+  done
+  python scripts/trunk_traffic.py $OUT/hbm_1 $OUT/hbm_2 "gpurun_out/r06k: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on scripts/trunk_heads_one.py 1024 20, dispatches 6-20 averaged" > profiles/trunk_traffic.json || exit $?
+  cp profiles/trunk_traffic.json $OUT/trunk_traffic.json
+  run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_default 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
+  rm -f $OUT/prof/run_kernel_trace.csv
+  exit 0
+}
+
+f3() {
+  # the other workloads' lines on the current tree
+  export OUT=gpurun_out/r06l
+  mkdir -p $OUT
+  run bench_c2 400 python bench.py --workload c2 --skip-cpu || exit $?
+  run bench_c4 400 python bench.py --workload c4 --skip-cpu --skip-kernel || exit $?
+  run bench_c5 400 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+  run bench_arena 400 python bench.py --workload arena || exit $?
+  exit 0
+}
 "$@"

@@ -34,3 +34,14 @@ def test_bench_configs2_leaf_batch(monkeypatch, argv, games, pipes):
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
     a = bench.parse()
     assert (a.games, a.pipelines) == (games, pipes)
+
+
+def test_bench_window_protocol_defaults(monkeypatch):
+    """The driver's command (--steps 20 --warmup 5) gets the sustained block and the settle
+    windows between the warmup and the timed window."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--warmup", "5"])
+    a = bench.parse()
+    assert (a.steps, a.warmup, a.settle, a.sustained_steps) == (20, 5, 3, 2000)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--settle", "0", "--sustained-steps", "0"])
+    a = bench.parse()
+    assert (a.settle, a.sustained_steps) == (0, 0)
