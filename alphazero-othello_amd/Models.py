@@ -713,12 +713,12 @@ class FusedInferenceNet(nn.Module, Inference):
                 and isinstance(self.stem, _HipStem) and self._fused_heads_ready()
                 and os.environ.get("AZ_W4_BOARDS", "2") == "2"):
             return False
+        if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16"
+                   and c.channels == 128 for c in convs):
+            return False
         # more boards than are resident at once run one launch per chunk: AZ_TRUNK4_CHUNKS=0
         # turns that off here as for the fp16x2 trunk (per-layer launches instead)
         if B > self._trunk4_cap(convs[0].wq.device) and not self.trunk4_chunks:
-            return False
-        if not all(getattr(c, "algo", "") == "wino4" and c.precision == "fp16"
-                   and c.channels == 128 for c in convs):
             return False
         if not hasattr(self, "_t4"):
             dev = convs[0].wq.device

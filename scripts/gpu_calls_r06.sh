@@ -204,6 +204,10 @@ f3() {
   run bench_c4 400 python bench.py --workload c4 --skip-cpu --skip-kernel || exit $?
   run bench_c5 400 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
   run bench_arena 400 python bench.py --workload arena || exit $?
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
   exit 0
 }
 "$@"
