@@ -868,6 +868,35 @@ class FusedInferenceNet(nn.Module, Inference):
                                 gshift=15 - e, gS=self.fast_gemm_splits)
         return True
 
+    # AZ_FAST_TRUNK (default on): FastOthelloNet's stem + residual block + conv_add in FP16X2 as
+    # ONE launch (az_fast_trunk_gpu: the activations between the convs stay in LDS; bit-identical
+    # to the three stem-fused / plain direct conv launches); 0 = the three launches
+    fuse_fast_trunk = os.environ.get("AZ_FAST_TRUNK", "1") == "1"
+
+    def _fast_trunk_ready(self):
+        if not (self.kind == "fast" and self.conv_impl == "hip" and self.fuse_fast_trunk
+                and self.fuse_stem and isinstance(self.stem, _HipStem) and len(self.c1) == 1):
+            return False
+        convs = [self.c1[0], self.c2[0], self.tail]
+        return all(getattr(c, "precision", "") == "fp16x2" and c.algo == "direct"
+                   and c.channels == 64 for c in convs)
+
+    def _fast_trunk(self, planes):
+        """The tail conv's output (NHWC [B, 64, 8, 8]) from canonical planes [B, 64] in one
+        launch (az_fast_trunk_gpu)."""
+        import az_native as nat
+
+        B = planes.shape[0]
+        planes = planes.reshape(B, 64).contiguous()
+        t = torch.empty((B, 64, 8, 8), dtype=torch.float32, device=planes.device,
+                        memory_format=torch.channels_last)
+        c1, c2, c3 = self.c1[0], self.c2[0], self.tail
+        nat.check(nat.lib.az_fast_trunk_gpu(
+            nat.ptr(planes), nat.ptr(self.stem.w9), nat.ptr(self.stem.bias), nat.ptr(c1.wq),
+            nat.ptr(c1.bias), nat.ptr(c2.wq), nat.ptr(c2.bias), nat.ptr(c3.wq), nat.ptr(c3.bias),
+            nat.ptr(t), B, 64, c1.mode, nat.stream_ptr()), "az_fast_trunk_gpu")
+        return t
+
     # AZ_FAST_GEMM (default on): the heads GEMM on az_heads_fast_gemm_gpu (fp16x2 MFMA, split
     # over AZ_FAST_GEMM_SPLITS = 8 slices of the 4,096 features) instead of torch.bmm (fp32)
     fast_gemm = os.environ.get("AZ_FAST_GEMM", "1") == "1"
@@ -885,7 +914,10 @@ class FusedInferenceNet(nn.Module, Inference):
 
             B = planes.shape[0]
             fw = self._fw
-            t = self.tail(self._trunk(planes.view(B, 1, 8, 8)))
+            if self._fast_trunk_ready():
+                t = self._fast_trunk(planes)
+            else:
+                t = self.tail(self._trunk(planes.view(B, 1, 8, 8)))
             hf = t.permute(0, 2, 3, 1).reshape(B, -1)  # a view of the channels-last output
             if "gq" in fw:
                 S = fw["gS"]

@@ -199,6 +199,60 @@ __device__ __forceinline__ float4 stem4(const float* pl, int p, const float4 (&s
   return make_float4(fmaxf(acc.x, 0.f), fmaxf(acc.y, 0.f), fmaxf(acc.z, 0.f), fmaxf(acc.w, 0.f));
 }
 
+// The main loop of one conv: 9 taps x C/16 chunks of 16 input channels, A fragments from the
+// staged image lds_a, B (weights) streamed three steps ahead through the ring b0f..b3f (the
+// first three requested by the caller: steps 0, 1, 2); acc is zeroed here.
+template <class G>
+__device__ __forceinline__ void mx_kloop(f32x16 (&acc)[G::TM], const char* lds_a, const char* wq,
+                                         int wlane, const int (&pos0)[G::TM],
+                                         const int (&ok9)[G::TM], int h, BFrag<G>& b0f,
+                                         BFrag<G>& b1f, BFrag<G>& b2f, BFrag<G>& b3f) {
+  constexpr int last = G::STEPS - 1;
+#pragma unroll
+  for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[mi][k] = 0.0f;
+
+  // Step s = (tap, chunk): MFMAs on A set s%2 and B set s%4; the A set of step s+1 is read
+  // meanwhile (next tap's row offsets precomputed at the tap's start) and B set (s+3)%4 —
+  // consumed by step s-1 — reloaded with step s+3.  Indices are clamped to the last step
+  // so every load is unconditional (exact vmcnt bookkeeping); surplus loads are unused.
+  // The machine scheduler would put a step's loads in one burst ahead of its MFMAs (the
+  // MFMA pipe then idles while they issue) or sink them behind; mx_sched pins the issue
+  // pattern: each LDS read in the shadow of two MFMAs, the weight loads behind the MFMAs.
+  static_assert(G::CHUNKS % 4 == 0, "B ring of 4 and A ring of 2 within a tap");
+  AFrag<G> a0f, a1f;
+  int bcur[G::TM], bnxt[G::TM];
+  mx_tap_base<G>(bcur, 0, pos0, ok9, h);
+  mx_read_a<G>(a0f, lds_a, bcur, 0);
+#define AZ_MX_STEP(CH, AC, AN, BC, BL)                                              \
+  {                                                                                 \
+    const int s_ = tap * G::CHUNKS + (CH);                                          \
+    if (!(AZ_MX_EXP & 1)) {                                                         \
+      if ((CH) + 1 < G::CHUNKS)                                                     \
+        mx_read_a<G>(AN, lds_a, bcur, (CH) + 1);                                    \
+      else                                                                          \
+        mx_read_a<G>(AN, lds_a, bnxt, 0);                                           \
+    }                                                                               \
+    mx_mma<G>(acc, AC, BC);                                                         \
+    if (!(AZ_MX_EXP & 2)) mx_load_b<G>(BL, wq, wlane, s_ + 3 < last ? s_ + 3 : last); \
+    mx_sched<G>();                                                                  \
+  }
+  for (int tap = 0; tap < 9; ++tap) {
+    mx_tap_base<G>(bnxt, tap + 1 < 9 ? tap + 1 : 8, pos0, ok9, h);
+#pragma unroll
+    for (int c4 = 0; c4 < G::CHUNKS; c4 += 4) {
+      AZ_MX_STEP(c4 + 0, a0f, a1f, b0f, b3f)
+      AZ_MX_STEP(c4 + 1, a1f, a0f, b1f, b0f)
+      AZ_MX_STEP(c4 + 2, a0f, a1f, b2f, b1f)
+      AZ_MX_STEP(c4 + 3, a1f, a0f, b3f, b2f)
+    }
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi) bcur[mi] = bnxt[mi];
+  }
+#undef AZ_MX_STEP
+}
+
 template <class G, bool RES, bool RELU, int STEM>
 __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restrict__ x,
                                                            const char* __restrict__ wq,
@@ -216,7 +270,6 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
   const int col0 = wave * 32;
   const int b0 = blockIdx.x * kBoards;
   const int nb = n_boards - b0 < kBoards ? n_boards - b0 : kBoards;
-  constexpr int last = G::STEPS - 1;
   // FP16X2: each staged board's max |x| (float bits: non-negative floats order as unsigned)
   __shared__ unsigned s_amax[kBoards];
   if (G::SCALED) {
@@ -349,52 +402,10 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
     ok9[mi] = ok;
   }
 
-  f32x16 acc[G::TM];
-#pragma unroll
-  for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc[mi][k] = 0.0f;
-
-  // Step s = (tap, chunk): MFMAs on A set s%2 and B set s%4; the A set of step s+1 is read
-  // meanwhile (next tap's row offsets precomputed at the tap's start) and B set (s+3)%4 —
-  // consumed by step s-1 — reloaded with step s+3.  Indices are clamped to the last step
-  // so every load is unconditional (exact vmcnt bookkeeping); surplus loads are unused.
-  // The machine scheduler would put a step's loads in one burst ahead of its MFMAs (the
-  // MFMA pipe then idles while they issue) or sink them behind; mx_sched pins the issue
-  // pattern: each LDS read in the shadow of two MFMAs, the weight loads behind the MFMAs.
-  static_assert(G::CHUNKS % 4 == 0, "B ring of 4 and A ring of 2 within a tap");
   const uint64_t clk0 = (AZ_MX_EXP & 16) ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t rt0 = (AZ_MX_EXP & 16) ? __builtin_amdgcn_s_memrealtime() : 0;
-  AFrag<G> a0f, a1f;
-  int bcur[G::TM], bnxt[G::TM];
-  mx_tap_base<G>(bcur, 0, pos0, ok9, h);
-  mx_read_a<G>(a0f, lds_a, bcur, 0);
-#define AZ_MX_STEP(CH, AC, AN, BC, BL)                                              \
-  {                                                                                 \
-    const int s_ = tap * G::CHUNKS + (CH);                                          \
-    if (!(AZ_MX_EXP & 1)) {                                                         \
-      if ((CH) + 1 < G::CHUNKS)                                                     \
-        mx_read_a<G>(AN, lds_a, bcur, (CH) + 1);                                    \
-      else                                                                          \
-        mx_read_a<G>(AN, lds_a, bnxt, 0);                                           \
-    }                                                                               \
-    mx_mma<G>(acc, AC, BC);                                                         \
-    if (!(AZ_MX_EXP & 2)) mx_load_b<G>(BL, wq, wlane, s_ + 3 < last ? s_ + 3 : last); \
-    mx_sched<G>();                                                                  \
-  }
-  for (int tap = 0; tap < 9; ++tap) {
-    mx_tap_base<G>(bnxt, tap + 1 < 9 ? tap + 1 : 8, pos0, ok9, h);
-#pragma unroll
-    for (int c4 = 0; c4 < G::CHUNKS; c4 += 4) {
-      AZ_MX_STEP(c4 + 0, a0f, a1f, b0f, b3f)
-      AZ_MX_STEP(c4 + 1, a1f, a0f, b1f, b0f)
-      AZ_MX_STEP(c4 + 2, a0f, a1f, b2f, b1f)
-      AZ_MX_STEP(c4 + 3, a1f, a0f, b3f, b2f)
-    }
-#pragma unroll
-    for (int mi = 0; mi < G::TM; ++mi) bcur[mi] = bnxt[mi];
-  }
-#undef AZ_MX_STEP
+  f32x16 acc[G::TM];
+  mx_kloop<G>(acc, lds_a, wq, wlane, pos0, ok9, h, b0f, b1f, b2f, b3f);
   if ((AZ_MX_EXP & 16) && blockIdx.x == 0 && tid == 0) {
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
     reinterpret_cast<uint64_t*>(y)[0] = clk1 - clk0;
@@ -467,6 +478,193 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
         y[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C] = v;
       }
     }
+  }
+}
+
+// FastOthelloNet's whole conv trunk in one launch (az_fast_trunk_gpu): stem -> residual block
+// (conv1, conv2 + stem residual) -> conv_add, one board per workgroup, FP16X2.  The same
+// arithmetic as the three az_conv3x3_mx_stem_gpu / az_conv3x3_mx_gpu launches (stem values,
+// per-board max, split, main loop, epilogue), so the output is bit-identical; what goes is the
+// two intermediate activations' HBM round trips and two launches: each conv's epilogue reduces
+// its output's max over the workgroup and writes the next conv's fp16 hi / lo image straight
+// into LDS from its registers.
+struct FastTrunkArgs {
+  const float* planes;  // [n][64] canonical boards
+  const float* stem_w;  // [9][C]
+  const float* stem_b;  // [C]
+  const char* wq[3];    // conv1, conv2, conv_add weights (az_conv3x3_mx_prep_gpu, FP16X2)
+  const float* bias[3];
+  float* y;             // NHWC [n][64][C]: conv_add's output
+  int n_boards;
+};
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
+  static_assert(G::BOARDS == 1 && G::SCALED, "one board per workgroup, FP16X2");
+  constexpr int C = G::C, kThreads = G::THREADS;
+  extern __shared__ float4 lds4[];
+  __shared__ float s_plane[100];
+  __shared__ unsigned s_amax[G::WAVES];
+  char* lds_a = reinterpret_cast<char*>(lds4);
+  // R: the stem output (conv2's residual), fp32 [64 positions][kRS] after the A image (rows
+  // padded to 72 floats: an epilogue access's two row groups, four rows apart, hit different
+  // banks)
+  constexpr int kRS = C + 8;
+  float* lds_r = reinterpret_cast<float*>(lds_a + G::LDS_BYTES);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int col0 = wave * 32, co = col0 + r;
+  const int b = blockIdx.x;
+  const int wlane = (col0 + r) * 32 + h * 16;
+  BFrag<G> b0f, b1f, b2f, b3f;
+  mx_load_b<G>(b0f, a.wq[0], wlane, 0);
+  mx_load_b<G>(b1f, a.wq[0], wlane, 1);
+  mx_load_b<G>(b2f, a.wq[0], wlane, 2);
+
+  // ---- conv1's input: stem(planes), staged as k_conv3x3_mx<STEM = 1> stages it
+  for (int i = tid; i < 100; i += kThreads) {
+    const int yy = i / 10 - 1, xx = i % 10 - 1;
+    s_plane[i] = (unsigned)yy < 8u && (unsigned)xx < 8u ? a.planes[(size_t)b * 64 + yy * 8 + xx]
+                                                        : 0.f;
+  }
+  if (tid < G::WAVES) s_amax[tid] = 0u;
+  __syncthreads();
+  int e_in;  // the current conv's input: max |x| < 2^e_in
+  {
+    constexpr int V = 65 * C / 4, ITER = (V + kThreads - 1) / kThreads;
+    static_assert(kThreads % (C / 4) == 0, "one channel quad per thread");
+    const int c = (tid % (C / 4)) * 4;
+    float4 stw[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) stw[t] = *reinterpret_cast<const float4*>(a.stem_w + t * C + c);
+    const float4 stb = *reinterpret_cast<const float4*>(a.stem_b + c);
+    float4 val[ITER];
+    unsigned m = 0u;
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      val[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (v < 64 * (C / 4)) {
+        val[i] = stem4(s_plane, v / (C / 4), stw, stb);
+        *reinterpret_cast<float4*>(lds_r + (v / (C / 4)) * kRS + (v % (C / 4)) * 4) = val[i];
+      }
+      m = max(m, max(max(__float_as_uint(fabsf(val[i].x)), __float_as_uint(fabsf(val[i].y))),
+                     max(__float_as_uint(fabsf(val[i].z)), __float_as_uint(fabsf(val[i].w)))));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+    if (lane == 0) s_amax[wave] = m;
+    __syncthreads();
+    unsigned mb = s_amax[0];
+#pragma unroll
+    for (int w = 1; w < G::WAVES; ++w) mb = max(mb, s_amax[w]);
+    const int be = (int)((mb >> 23) & 0xff);
+    e_in = be == 0 ? 0 : be - 126;
+    const float xsc = ldexpf(1.0f, 15 - e_in);
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int v = tid + i * kThreads;
+      if (v >= V) continue;
+      char* dst = lds_a + (v / (C / 4)) * G::APOS + (v % (C / 4)) * 8;
+      const f32x4 x4 = {val[i].x, val[i].y, val[i].z, val[i].w};
+      const f32x4 as = x4 * xsc;
+      const f16x4 hi = __builtin_convertvector(as, f16x4);
+      const f16x4 lo = __builtin_convertvector(as - __builtin_convertvector(hi, f32x4), f16x4);
+      *reinterpret_cast<f16x4*>(dst) = hi;
+      *reinterpret_cast<f16x4*>(dst + C * 2) = lo;
+    }
+  }
+  __syncthreads();
+
+  int pos0[G::TM], ok9[G::TM];
+#pragma unroll
+  for (int mi = 0; mi < G::TM; ++mi) {
+    const int m = 32 * mi + r;
+    const int py = (m >> 3) & 7, px = m & 7;
+    pos0[mi] = m;
+    int ok = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+      ok |= ((unsigned)yy < 8u && (unsigned)xx < 8u) << t;
+    }
+    ok9[mi] = ok;
+  }
+
+  f32x16 acc[G::TM];
+#pragma unroll  // three bodies: 116 VGPRs, three waves per SIMD (one body: 156, two)
+  for (int layer = 0; layer < 3; ++layer) {
+    const char* wq = a.wq[layer];
+    mx_kloop<G>(acc, lds_a, wq, wlane, pos0, ok9, h, b0f, b1f, b2f, b3f);
+    // epilogue (k_conv3x3_mx's): v = acc * 2^-(sx + sw) + bias (+ stem residual), ReLU
+    const int sw = reinterpret_cast<const int*>(wq + G::W_BYTES)[1];
+    const float osc = ldexpf(1.0f, -(15 - e_in) - sw);
+    const float bv = a.bias[layer][co];
+    f32x16(&v)[G::TM] = acc;  // the epilogue's values replace the accumulators in place
+    if (layer == 1) {  // residual = the stem output kept in R (the same values the separate
+                       // conv2's recomputation gives: stem4's chain is k_conv3x3_mx<STEM = 2>'s)
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int m = 32 * mi + (k & 3) + 8 * (k >> 2) + 4 * h;
+          float x = v[mi][k] * osc + bv;
+          x += lds_r[m * kRS + co];
+          v[mi][k] = fmaxf(x, 0.0f);
+        }
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[mi][k] = fmaxf(v[mi][k] * osc + bv, 0.0f);
+    }
+    if (layer == 2) {  // conv_add's output: NHWC to global memory
+      if (b < a.n_boards) {
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi) {
+          const size_t o0 = ((size_t)b * 64 + 32 * mi + 4 * h) * C + co;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) a.y[o0 + (size_t)((k & 3) + 8 * (k >> 2)) * C] = v[mi][k];
+        }
+      }
+      break;
+    }
+    // the next conv's input image: the board's max over every wave's values (this barrier
+    // also ends every wave's reads of the current image), then hi / lo words from registers
+    unsigned m = 0u;
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m = max(m, __float_as_uint(fabsf(v[mi][k])));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+    __syncthreads();  // the previous image's maxima read, every wave's main loop done
+    if (lane == 0) s_amax[wave] = m;
+    __syncthreads();
+    unsigned mb = s_amax[0];
+#pragma unroll
+    for (int w = 1; w < G::WAVES; ++w) mb = max(mb, s_amax[w]);
+    const int be = (int)((mb >> 23) & 0xff);
+    e_in = be == 0 ? 0 : be - 126;
+    const float xsc = ldexpf(1.0f, 15 - e_in);
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int m = 32 * mi + (k & 3) + 8 * (k >> 2) + 4 * h;
+        const float s = v[mi][k] * xsc;  // exact: a power of two
+        const _Float16 hi = (_Float16)s;
+        const _Float16 lo = (_Float16)(s - (float)hi);
+        char* dst = lds_a + m * G::APOS + co * 2;
+        *reinterpret_cast<_Float16*>(dst) = hi;
+        *reinterpret_cast<_Float16*>(dst + C * 2) = lo;
+      }
+    // the next conv's first weight steps, in flight across the barrier
+    mx_load_b<G>(b0f, a.wq[layer + 1], wlane, 0);
+    mx_load_b<G>(b1f, a.wq[layer + 1], wlane, 1);
+    mx_load_b<G>(b2f, a.wq[layer + 1], wlane, 2);
+    __syncthreads();
   }
 }
 
@@ -663,4 +861,29 @@ extern "C" int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w,
   return launch_mx_cfg(role == 1 ? stem_b : x, wq, bias, role == 2 ? stem_b : nullptr, y,
                        n_boards, channels, 1, mode, mx_default_cfg(), azc::as_stream(stream), st,
                        role);
+}
+
+extern "C" int az_fast_trunk_gpu(const float* planes, const float* stem_w, const float* stem_b,
+                                 const void* wq1, const float* bias1, const void* wq2,
+                                 const float* bias2, const void* wq3, const float* bias3,
+                                 float* y, int32_t n_boards, int32_t channels, int32_t mode,
+                                 void* stream) {
+  AZ_REQUIRE(n_boards >= 0, AZ_ERR_ARG, "az_fast_trunk_gpu: n_boards < 0");
+  if (n_boards == 0) return AZ_OK;
+  AZ_REQUIRE(channels == 64 && mode == AZ_CONV_FP16X2, AZ_ERR_ARG,
+             "az_fast_trunk_gpu: 64 channels in FP16X2 only (got %d / mode %d)", channels, mode);
+  AZ_REQUIRE(planes && stem_w && stem_b && wq1 && bias1 && wq2 && bias2 && wq3 && bias3 && y,
+             AZ_ERR_ARG, "az_fast_trunk_gpu: null buffer");
+  AZ_REQUIRE(((uintptr_t)stem_w | (uintptr_t)stem_b | (uintptr_t)wq1 | (uintptr_t)wq2 |
+              (uintptr_t)wq3) % 16 == 0,
+             AZ_ERR_ARG, "az_fast_trunk_gpu: buffers must be 16-byte aligned");
+  using G = Mx<64, AZ_CONV_FP16X2, 1>;
+  const FastTrunkArgs a{planes, stem_w, stem_b,
+                        {static_cast<const char*>(wq1), static_cast<const char*>(wq2),
+                         static_cast<const char*>(wq3)},
+                        {bias1, bias2, bias3}, y, n_boards};
+  hipLaunchKernelGGL(k_fast_trunk<G>, dim3((unsigned)n_boards), dim3(G::THREADS),
+                     G::LDS_BYTES + 64 * (64 + 8) * 4, azc::as_stream(stream), a);
+  AZ_HIP(hipGetLastError());
+  return AZ_OK;
 }

@@ -375,6 +375,21 @@ int az_conv3x3_mx_stem_gpu(const float* planes, const float* stem_w, const float
                            int32_t n_boards, int32_t channels, int32_t role, int32_t mode,
                            void* stream);
 
+/* FastOthelloNet's whole conv trunk in one launch (csrc/conv16.hip, k_fast_trunk): the stem
+ * (planes float [n_boards][64], stem_w [9][64], stem_b [64]), the residual block's conv1
+ * (wq1 / bias1) and conv2 (wq2 / bias2, + the stem output, ReLU) and conv_add (wq3 / bias3),
+ * each conv + bias + ReLU in FP16X2 (weights from az_conv3x3_mx_prep_gpu with
+ * AZ_CONV_FP16X2); y NHWC float [n_boards][64][64] = conv_add's output.  One board per
+ * workgroup: the activations between the convs stay in LDS (each epilogue writes the next
+ * conv's fp16 hi / lo image from its registers), bit-identical to az_conv3x3_mx_stem_gpu
+ * (role 1), az_conv3x3_mx_stem_gpu (role 2) and az_conv3x3_mx_gpu in sequence.  channels must
+ * be 64 and mode AZ_CONV_FP16X2.  Replaces initial_conv, res_block and conv_add
+ * (Models.py:103-116, 144-146). */
+int az_fast_trunk_gpu(const float* planes, const float* stem_w, const float* stem_b,
+                      const void* wq1, const float* bias1, const void* wq2, const float* bias2,
+                      const void* wq3, const float* bias3, float* y, int32_t n_boards,
+                      int32_t channels, int32_t mode, void* stream);
+
 /* The same convolution as Winograd F(2x2, 3x3) (csrc/conv_wino.hip): 2.25x fewer MFMA
  * products; the input/output transforms only add and subtract and the weight transform
  * G g G^T is done once in fp64, so SPLIT3 stays at the direct fp32 kernel's error (the

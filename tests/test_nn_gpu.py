@@ -622,3 +622,31 @@ def test_heads_fast_gemm_is_fp32_accurate(B, splits):
     for bi in range(B):
         assert e_g[bi].max() <= 2 * e_32[bi].max() + 1e-7 * (1 + ref[bi].abs().max()), bi
     assert FusedInferenceNet.fast_gemm_splits in (4, 8)
+
+
+@pytest.mark.parametrize("B", [1, 7, 300, 2048])
+def test_fast_trunk_bit_identical_to_three_launches(B, monkeypatch):
+    """az_fast_trunk_gpu (FastOthelloNet's stem, residual block and conv_add in one launch,
+    the activations between the convs kept in LDS) against the three stem-fused / plain direct
+    FP16X2 conv launches: the tail output bit for bit, and the priors / values of the fused
+    evaluation path the engine runs."""
+    from Models import FusedInferenceNet
+
+    torch.manual_seed(11)
+    net = FastOthelloNet(8, 65).cuda().eval()
+    fused = inference_copy(net, "cuda")
+    assert fused._fast_trunk_ready()
+    x = torch.randint(-1, 2, (B, 64), device="cuda").float()
+    with torch.no_grad():
+        a = fused._fast_trunk(x)
+        b = fused.tail(fused._trunk(x.view(B, 1, 8, 8)))
+        out = {}
+        for flag in (True, False):
+            monkeypatch.setattr(FusedInferenceNet, "fuse_fast_trunk", flag)
+            pr = torch.empty(B, 65, device="cuda")
+            va = torch.empty(B, device="cuda")
+            fused.evaluate_into(x, pr, va)
+            out[flag] = (pr, va)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
