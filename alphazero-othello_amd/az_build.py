@@ -39,6 +39,22 @@ def source_hash():
     return h.hexdigest()
 
 
+# the persistent trunk's kernel sources: what profiles/trunk_traffic.json's PMC figure depends
+# on (the az_othello.h declarations and the other kernels do not change its code)
+TRUNK_SOURCES = ["csrc/conv_wino4.hip", "csrc/heads_az.h", "csrc/common.h"]
+
+
+def sources_hash(files):
+    """sha256 over the flags and the given sources (name and bytes), in the given order."""
+    h = hashlib.sha256()
+    h.update(" ".join(FLAGS).encode())
+    for f in files:
+        h.update(b"\0" + f.encode() + b"\0")
+        with open(os.path.join(HERE, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def built_id(path=OUT):
     """The AZ_BUILD_ID embedded in a built library (read from the file, not loaded)."""
     if not os.path.exists(path):

@@ -477,22 +477,26 @@ def trunk_roofline(sp, device, n_boards):
                 + 2 * 128 * 65 + 2 * 64 * 256 + 2 * 256)
     algorithmic = per_eval * n_boards / (ms * 1e-3) / 1e12
     # HBM bytes per launch from the committed PMC summary (scripts/trunk_traffic.py), used only
-    # for the build it was measured on: the file records the library's source hash, and a
-    # kernel change makes the figure stale (reported as such, traffic null)
+    # while the trunk kernel is the one it was measured on: the file records the hash of the
+    # trunk's sources, and the loaded library must be the build of the tree's sources (a kernel
+    # change makes the figure stale: reported as such, traffic null)
     traffic, source = None, None
     tj = os.path.join(ROOT, "profiles", "trunk_traffic.json")
     if n_boards == 1024 and prec == "fp16x2" and os.path.exists(tj):
         try:
+            import az_build
             import az_native as nat
 
             tjd = json.load(open(tj))
-            current = nat.build_id()
+            kernel = az_build.sources_hash(az_build.TRUNK_SOURCES)
             source = {"file": "profiles/trunk_traffic.json", "measured": tjd.get("source"),
-                      "build_id": tjd.get("build_id"), "current_build_id": current}
-            if tjd.get("build_id") == current:
+                      "trunk_sources_hash": tjd.get("trunk_sources_hash"),
+                      "current_trunk_sources_hash": kernel,
+                      "library_is_tree_build": nat.build_id() == az_build.source_hash()}
+            if tjd.get("trunk_sources_hash") == kernel and source["library_is_tree_build"]:
                 traffic = tjd.get("hbm_bytes_per_launch")
             else:
-                source["stale"] = "measured on another build of the library: not reported"
+                source["stale"] = "measured on another trunk kernel: not reported"
         except (OSError, ValueError):
             traffic = None
     fn = "az_trunk_wino4_heads_gpu" if prec == "fp16x2" else "az_trunk_wino4_heads_fp16_gpu"

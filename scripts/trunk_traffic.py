@@ -1,6 +1,7 @@
 """profiles/trunk_traffic.json from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over
 scripts/trunk_heads_one.py 1024 20 (the launch bench.py's roofline_trunk times), with the
-library's source hash, so bench.py reports the figure only for the build it was measured on.
+hash of the trunk kernel's sources (and the library's), so bench.py reports the figure only while
+the kernel is the one it was measured on.
     python scripts/trunk_traffic.py <fetch pass dir> <write pass dir> <source note> > profiles/trunk_traffic.json
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of wide
 reads -> x 2 (checked on the calibration copy in profiles/oth_step_traffic.json); WRITE_SIZE as
@@ -36,6 +37,7 @@ def main():
         "kernel": "k_trunk_wino4<..., heads> (az_trunk_wino4_heads_gpu: stem + 10 block convs + "
                   "heads, the layer input resident in LDS), the launch bench.py's roofline_trunk times",
         "boards": 1024, "source": sys.argv[3], "build_id": az_build.source_hash(),
+        "trunk_sources_hash": az_build.sources_hash(az_build.TRUNK_SOURCES),
         "dispatches_averaged": [nf, nw],
         "FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
         "correction": "gfx950: FETCH_SIZE counts half the bytes of wide reads -> x 2 "
