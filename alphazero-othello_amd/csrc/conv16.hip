@@ -487,7 +487,8 @@ __global__ __launch_bounds__(G::THREADS) void k_conv3x3_mx(const float* __restri
 // per-board max, split, main loop, epilogue), so the output is bit-identical; what goes is the
 // two intermediate activations' HBM round trips and two launches: each conv's epilogue reduces
 // its output's max over the workgroup and writes the next conv's fp16 hi / lo image straight
-// into LDS from its registers.
+// into LDS from its registers; conv2's residual (the stem output) is recomputed in its
+// epilogue, as the separate stem-fused conv does.
 struct FastTrunkArgs {
   const float* planes;  // [n][64] canonical boards
   const float* stem_w;  // [9][C]
@@ -506,11 +507,6 @@ __global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
   __shared__ float s_plane[100];
   __shared__ unsigned s_amax[G::WAVES];
   char* lds_a = reinterpret_cast<char*>(lds4);
-  // R: the stem output (conv2's residual), fp32 [64 positions][kRS] after the A image (rows
-  // padded to 72 floats: an epilogue access's two row groups, four rows apart, hit different
-  // banks)
-  constexpr int kRS = C + 8;
-  float* lds_r = reinterpret_cast<float*>(lds_a + G::LDS_BYTES);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -545,10 +541,7 @@ __global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
     for (int i = 0; i < ITER; ++i) {
       const int v = tid + i * kThreads;
       val[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (v < 64 * (C / 4)) {
-        val[i] = stem4(s_plane, v / (C / 4), stw, stb);
-        *reinterpret_cast<float4*>(lds_r + (v / (C / 4)) * kRS + (v % (C / 4)) * 4) = val[i];
-      }
+      if (v < 64 * (C / 4)) val[i] = stem4(s_plane, v / (C / 4), stw, stb);
       m = max(m, max(max(__float_as_uint(fabsf(val[i].x)), __float_as_uint(fabsf(val[i].y))),
                      max(__float_as_uint(fabsf(val[i].z)), __float_as_uint(fabsf(val[i].w)))));
     }
@@ -602,15 +595,24 @@ __global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
     const float osc = ldexpf(1.0f, -(15 - e_in) - sw);
     const float bv = a.bias[layer][co];
     f32x16(&v)[G::TM] = acc;  // the epilogue's values replace the accumulators in place
-    if (layer == 1) {  // residual = the stem output kept in R (the same values the separate
-                       // conv2's recomputation gives: stem4's chain is k_conv3x3_mx<STEM = 2>'s)
+    if (layer == 1) {  // residual = stem(planes) at (row, co): k_conv3x3_mx<STEM = 2>'s chain
+      // (recomputed: an fp32 copy in LDS would cost occupancy -- 4 workgroups per CU by LDS
+      // instead of 6 by registers; A/B: profiles/r06_c2_fast_trunk_ab.json)
 #pragma unroll
       for (int mi = 0; mi < G::TM; ++mi)
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const int m = 32 * mi + (k & 3) + 8 * (k >> 2) + 4 * h;
+          const int py = (m >> 3) & 7, px = m & 7;
+          float rs = a.stem_b[co];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+            if ((unsigned)yy < 8u && (unsigned)xx < 8u)
+              rs = fmaf(s_plane[(yy + 1) * 10 + xx + 1], a.stem_w[t * C + co], rs);
+          }
           float x = v[mi][k] * osc + bv;
-          x += lds_r[m * kRS + co];
+          x += fmaxf(rs, 0.f);
           v[mi][k] = fmaxf(x, 0.0f);
         }
     } else {
@@ -882,8 +884,8 @@ extern "C" int az_fast_trunk_gpu(const float* planes, const float* stem_w, const
                         {static_cast<const char*>(wq1), static_cast<const char*>(wq2),
                          static_cast<const char*>(wq3)},
                         {bias1, bias2, bias3}, y, n_boards};
-  hipLaunchKernelGGL(k_fast_trunk<G>, dim3((unsigned)n_boards), dim3(G::THREADS),
-                     G::LDS_BYTES + 64 * (64 + 8) * 4, azc::as_stream(stream), a);
+  hipLaunchKernelGGL(k_fast_trunk<G>, dim3((unsigned)n_boards), dim3(G::THREADS), G::LDS_BYTES,
+                     azc::as_stream(stream), a);
   AZ_HIP(hipGetLastError());
   return AZ_OK;
 }

@@ -228,4 +228,22 @@ c10() {
   rm -f $OUT/prof_c2/run_kernel_trace.csv
   exit 0
 }
+
+c11() {
+  # the fused FastOthelloNet trunk with conv2's residual recomputed (six workgroups per CU)
+  # against the LDS-copy form (exp6/ftR: four per CU by LDS) and the three launches
+  export OUT=gpurun_out/r06n
+  mkdir -p $OUT
+  pyt pytest_ft 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py -k "fast or stem_fusion" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_ldsR 300 env AZ_LIB_PATH=exp6/ftR/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_3l 300 env AZ_FAST_TRUNK=0 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000 --sustained-steps 0 --settle 0
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
 "$@"
