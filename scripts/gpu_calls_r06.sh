@@ -246,4 +246,24 @@ c11() {
   rm -f $OUT/prof_c2/run_kernel_trace.csv
   exit 0
 }
+
+fin() {
+  # the final tree: the whole GPU suite, smoke(), the driver's bench command and its kernel
+  # summary, the other workloads' lines and configs[1]'s kernel summary
+  export OUT=gpurun_out/r06o
+  mkdir -p $OUT
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+  run bench_c2 400 python bench.py --workload c2 --skip-cpu || exit $?
+  run bench_c4 400 python bench.py --workload c4 --skip-cpu --skip-kernel || exit $?
+  run bench_c5 400 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+  run bench_arena 400 python bench.py --workload arena || exit $?
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_default 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
+  rm -f $OUT/prof/run_kernel_trace.csv
+  exit 0
+}
 "$@"
