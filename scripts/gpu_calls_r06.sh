@@ -266,4 +266,16 @@ fin() {
   rm -f $OUT/prof/run_kernel_trace.csv
   exit 0
 }
+
+c12() {
+  # the trunk's MFMA shape alone: exp6/m16 (-DAZ_W4_EXP=1024, every 32x32x16 MFMA as two
+  # 16x16x32, wrong results, same FLOP and cycles) against the product, alternating
+  export OUT=gpurun_out/r06p
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run net_prod 120 python scripts/net_time.py 1024 40 || exit $?
+    run net_m16 120 env AZ_LIB_PATH=exp6/m16/libaz_othello.so python scripts/net_time.py 1024 40 || exit $?
+  done
+  exit 0
+}
 "$@"
