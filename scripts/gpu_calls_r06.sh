@@ -278,4 +278,18 @@ c12() {
   done
   exit 0
 }
+
+c13() {
+  # configs[3] / configs[4] as four 1,024-game pipelines (one 1,024-board evaluation each)
+  # against the two 2,048-game default
+  export OUT=gpurun_out/r06q
+  mkdir -p $OUT
+  for i in 1 2; do
+    run bench_c5 300 python bench.py --workload c5 --skip-cpu --skip-kernel || exit $?
+    run bench_c5_p4 300 python bench.py --workload c5 --skip-cpu --skip-kernel --pipelines 4 || exit $?
+    run bench_c4 300 python bench.py --workload c4 --skip-cpu --skip-kernel || exit $?
+    run bench_c4_p4 300 python bench.py --workload c4 --skip-cpu --skip-kernel --pipelines 4 || exit $?
+  done
+  exit 0
+}
 "$@"
