@@ -292,4 +292,15 @@ c13() {
   done
   exit 0
 }
+
+c14() {
+  # the driver's command three times on one more box (the window's spread)
+  export OUT=gpurun_out/r06r
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run bench_default_$i 600 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
+  done
+  run bench_8000 600 python bench.py --gpus 1 --steps 8000 --warmup 5 --skip-cpu --skip-kernel --settle 0 || exit $?
+  exit 0
+}
 "$@"
