@@ -303,4 +303,17 @@ c14() {
   run bench_8000 600 python bench.py --gpus 1 --steps 8000 --warmup 5 --skip-cpu --skip-kernel --settle 0 || exit $?
   exit 0
 }
+c15() {
+  # graph length vs the driver's 20-step window: 8 (default, 8 + 8 + four single-step
+  # replays per pipeline), 10 and 20 (divide the window), 4; four more windows per run
+  export OUT=gpurun_out/r06s
+  mkdir -p $OUT
+  export AZ_BENCH_REPEAT=4
+  for i in 1 2; do
+    for k in 8 10 20 4; do
+      run bench_spg${k}_$i 300 python bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --skip-kernel --steps-per-graph $k || exit $?
+    done
+  done
+  exit 0
+}
 "$@"
