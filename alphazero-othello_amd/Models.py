@@ -865,7 +865,8 @@ class FusedInferenceNet(nn.Module, Inference):
                 planes = torch.stack([p.view(64 * C // 16, 16, 128).permute(0, 2, 1)
                                       for p in (hi, lo)], 1).contiguous()  # [K/16][2][128][16]
                 self._fw.update(gq=planes.view(torch.int16), g128=wt[:, 128].contiguous(),
-                                gshift=15 - e, gS=self.fast_gemm_splits)
+                                gshift=15 - e, gS=self.fast_gemm_splits,
+                                gR=self.fast_gemm_tile)
         return True
 
     # AZ_FAST_TRUNK (default on): FastOthelloNet's stem + residual block + conv_add in FP16X2 as
@@ -901,6 +902,8 @@ class FusedInferenceNet(nn.Module, Inference):
     # over AZ_FAST_GEMM_SPLITS = 8 slices of the 4,096 features) instead of torch.bmm (fp32)
     fast_gemm = os.environ.get("AZ_FAST_GEMM", "1") == "1"
     fast_gemm_splits = int(os.environ.get("AZ_FAST_GEMM_SPLITS", "8"))
+    # boards per GEMM workgroup (32 R: each weight fragment feeds R row tiles)
+    fast_gemm_tile = int(os.environ.get("AZ_FAST_GEMM_TILE", "32"))
 
     def evaluate_into(self, planes, priors, values, stem_done=False):
         """Leaf evaluation straight into the engine's buffers: priors float32 [B, 65]
@@ -924,7 +927,8 @@ class FusedInferenceNet(nn.Module, Inference):
                 part = torch.empty(S, B, fw["ld"], dtype=torch.float32, device=hf.device)
                 nat.check(nat.lib.az_heads_fast_gemm_gpu(
                     nat.ptr(hf), nat.ptr(fw["gq"]), nat.ptr(fw["g128"]), fw["gshift"],
-                    nat.ptr(part), fw["ld"], S, B, nat.stream_ptr()), "az_heads_fast_gemm_gpu")
+                    nat.ptr(part), fw["ld"], S, fw["gR"], B, nat.stream_ptr()),
+                    "az_heads_fast_gemm_gpu")
             else:
                 S = fw["S"]
                 part = torch.bmm(hf.view(B, S, -1).transpose(0, 1), fw["wk"])  # [S, B, ld]

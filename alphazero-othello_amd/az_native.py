@@ -120,7 +120,7 @@ SIGNATURES = {
     "az_conv3x3_cfg_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_prep_gpu": [_P, _P, _I32, _I32, _P],
     "az_conv3x3_mx_prep_bytes": [_I32, _I32],
-    "az_heads_fast_gemm_gpu": [_P, _P, _P, _I32, _P, _I32, _I32, _I32, _P],
+    "az_heads_fast_gemm_gpu": [_P, _P, _P, _I32, _P, _I32, _I32, _I32, _I32, _P],
     "az_fast_trunk_gpu": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P],
     "az_conv3x3_mx_gpu": [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P],
     "az_conv3x3_wino_prep_gpu": [_P, _P, _I32, _I32, _P],

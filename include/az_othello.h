@@ -557,7 +557,7 @@ int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t parts, con
                              int32_t n_boards, void* stream);
 
 /* FastOthelloNet's heads GEMM before az_heads_fast_finish_gpu (csrc/heads.hip): part
- * [splits][n_boards][ld] float = the partial sums over `splits` (4 or 8) slices of K = 4,096 of
+ * [splits][n_boards][ld] float = the partial sums over `splits` slices of K = 4,096 of
  * x[b][k] * W[k][n] for the 129 columns [fc_policy; fc_value1] (columns 129 .. ld-1 zeroed),
  * fp32-accurate on the 16-bit MFMA pipe: x = the tail conv's NHWC output [n_boards][4,096]
  * (k = square * 64 + channel), each board's slice scaled by a power of two from its max |x|
@@ -565,10 +565,12 @@ int az_heads_fast_finish_gpu(const float* logits, int32_t ld, int32_t parts, con
  * into fp16 hi / lo words laid out [K/16][2][128][16] (16-byte aligned); w128 = column 128 of
  * W in fp32 [4,096] (fp32 FMAs).  Three MFMA products (lo*hi, hi*lo, hi*hi), fp32
  * accumulation, both scales removed exactly.  Replaces the reference's fc_policy / fc_value1
- * (Models.py:118-124, 150-156). */
+ * (Models.py:118-124, 150-156).  board_tile = boards per workgroup (32 R: each weight fragment
+ * feeds R MFMA row tiles); (board_tile, splits) one of (32, 4), (32, 8), (64, 8), (64, 16),
+ * (128, 16). */
 int az_heads_fast_gemm_gpu(const float* x, const void* wq, const float* w128, int32_t wshift,
-                           float* part, int32_t ld, int32_t splits, int32_t n_boards,
-                           void* stream);
+                           float* part, int32_t ld, int32_t splits, int32_t board_tile,
+                           int32_t n_boards, void* stream);
 
 /* stem: 1 -> channels 3x3 conv + bias + ReLU on canonical planes float [n_boards, 64];
  * w9: [9][channels]; y NHWC.  Replaces conv0+bn0+relu / initial_conv (Models.py:103-105,

@@ -316,4 +316,45 @@ c15() {
   done
   exit 0
 }
+c16() {
+  # FastOthelloNet's heads: the finish kernel's part loads issued together (product) against
+  # one part at a time (exp6/rolled), the GEMM's weight prefetch 6 steps ahead (exp6/pd6);
+  # tests, configs[1] A/B, kernel profile
+  export OUT=gpurun_out/r06t
+  mkdir -p $OUT
+  pyt pytest_heads 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py -k "fast or heads" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_rolled 300 env AZ_LIB_PATH=exp6/rolled/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_pd6 300 env AZ_LIB_PATH=exp6/pd6/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  run rocprof_c2 500 rocprofv3 --kernel-trace --stats \
+    --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000 --sustained-steps 0 --settle 0
+  rm -f $OUT/prof_c2/run_kernel_trace.csv
+  exit 0
+}
+c17() {
+  # c16 again on a consistent tree, plus the GEMM's board tile (AZ_FAST_GEMM_TILE 64 / 128: each
+  # weight fragment feeds 2 / 4 row tiles) at 8 / 16 K slices
+  export OUT=gpurun_out/r06u
+  mkdir -p $OUT
+  pyt pytest_heads 600 tests/test_nn_gpu.py tests/test_net_golden_gpu.py -k "fast or heads" || exit $?
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_rolled 300 env AZ_LIB_PATH=exp6/rolled/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_pd6 300 env AZ_LIB_PATH=exp6/pd6/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_t64s8 300 env AZ_FAST_GEMM_TILE=64 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_t64s16 300 env AZ_FAST_GEMM_TILE=64 AZ_FAST_GEMM_SPLITS=16 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_t128s16 300 env AZ_FAST_GEMM_TILE=128 AZ_FAST_GEMM_SPLITS=16 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+  for v in t32s8:32:8 t64s16:64:16 t128s16:128:16; do
+    IFS=: read n t sp <<< "$v"
+    run rocprof_c2_$n 500 env AZ_FAST_GEMM_TILE=$t AZ_FAST_GEMM_SPLITS=$sp rocprofv3 --kernel-trace --stats \
+      --output-format csv -d $OUT/prof_c2_$n -o run -- python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000 --sustained-steps 0 --settle 0 || exit $?
+    rm -f $OUT/prof_c2_$n/run_kernel_trace.csv
+  done
+  exit 0
+}
 "$@"

@@ -80,6 +80,16 @@ def test_cpu_illegal_reports_error():
     assert st[0] & nat.AZ_FLAG_ILLEGAL and o[0] == 0x0000000810000000
 
 
+def test_heads_fast_gemm_rejects_unbuilt_tiles():
+    """az_heads_fast_gemm_gpu checks (board_tile, splits) before it touches the device: an
+    unbuilt pair is an AZ_ERR_ARG naming both (the buffers are never dereferenced)."""
+    fake = 1 << 20  # 16-byte aligned, never read
+    rc = nat.lib.az_heads_fast_gemm_gpu(fake, fake, fake, 0, fake, 132, 8, 48, 1, None)
+    assert rc != nat.AZ_OK and "board_tile" in nat.last_error()
+    rc = nat.lib.az_heads_fast_gemm_gpu(fake, fake, fake, 0, fake, 132, 4, 64, 1, None)
+    assert rc != nat.AZ_OK and "(64, 4)" in nat.last_error()
+
+
 def test_pack_unpack_roundtrip_and_rotated_helpers():
     from envs.othello import OthelloGameNew
 

@@ -585,8 +585,8 @@ def test_trunk_heads_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [1, 33, 2048])
-@pytest.mark.parametrize("splits", [4, 8])
-def test_heads_fast_gemm_is_fp32_accurate(B, splits):
+@pytest.mark.parametrize("tile,splits", [(32, 4), (32, 8), (64, 8), (64, 16), (128, 16)])
+def test_heads_fast_gemm_is_fp32_accurate(B, tile, splits):
     """az_heads_fast_gemm_gpu (FastOthelloNet's heads GEMM on the 16-bit MFMA pipe, fp16 hi /
     lo operands after power-of-two scaling -- per board and slice for the features, per
     matrix for the weights -- three products, column 128 as fp32 FMAs) against fp64: the
@@ -594,7 +594,7 @@ def test_heads_fast_gemm_is_fp32_accurate(B, splits):
     1e-3 to 1e3), columns past 128 zero, a ragged last row tile."""
     from Models import FusedInferenceNet
 
-    g = torch.Generator().manual_seed(B * 7 + splits)
+    g = torch.Generator().manual_seed(B * 7 + splits + tile)
     x = torch.randn(B, 4096, generator=g).relu()
     if B > 1:
         x = x * torch.logspace(-3, 3, B).view(B, 1)
@@ -611,7 +611,7 @@ def test_heads_fast_gemm_is_fp32_accurate(B, splits):
     part = torch.full((splits, B, ld), float("nan"), device="cuda")
     nat.check(nat.lib.az_heads_fast_gemm_gpu(nat.ptr(xd), nat.ptr(wq.view(torch.int16)),
                                              nat.ptr(w128), 15 - e, nat.ptr(part), ld, splits,
-                                             B, nat.stream_ptr()), "az_heads_fast_gemm_gpu")
+                                             tile, B, nat.stream_ptr()), "az_heads_fast_gemm_gpu")
     torch.cuda.synchronize()
     assert torch.isfinite(part).all()
     assert (part[:, :, 129:] == 0).all()
@@ -621,7 +621,8 @@ def test_heads_fast_gemm_is_fp32_accurate(B, splits):
     assert e_g.max() <= 2 * e_32.max() + 1e-6, (e_g.max(), e_32.max())
     for bi in range(B):
         assert e_g[bi].max() <= 2 * e_32[bi].max() + 1e-7 * (1 + ref[bi].abs().max()), bi
-    assert FusedInferenceNet.fast_gemm_splits in (4, 8)
+    assert (FusedInferenceNet.fast_gemm_tile, FusedInferenceNet.fast_gemm_splits) in (
+        (32, 4), (32, 8), (64, 8), (64, 16), (128, 16))
 
 
 @pytest.mark.parametrize("B", [1, 7, 300, 2048])
