@@ -58,11 +58,13 @@ def allgather_samples(s, device, group=None):
     dist.all_gather(cnts, cnt, group=group)
     counts = [int(c.item()) for c in cnts]
     mx = max(counts) if counts else 0
+    if mx == 0:  # no rank has rows: every rank agrees from the counts, skip the empty collective
+        return unpack_rows(rows), counts
     pad = torch.zeros(mx, ROW_BYTES, dtype=torch.uint8, device=device)
     pad[:rows.shape[0]] = rows
     out = torch.empty(world * mx, ROW_BYTES, dtype=torch.uint8, device=device)
     dist.all_gather_into_tensor(out, pad, group=group)
-    keep = torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)]) if mx else out
+    keep = torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
     return unpack_rows(keep), counts
 
 

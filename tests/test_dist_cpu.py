@@ -26,7 +26,7 @@ def _rows(rank, n):
             "player": rng.choice([-1, 1], n).astype(np.int8)}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, counts=(5, 0, 3)):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "alphazero-othello_amd"))
@@ -36,7 +36,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    counts = [5, 0, 3][:world]
+    counts = list(counts)[:world]
     got, cnts = allgather_samples(_rows(rank, counts[rank]), "cpu")
     torch.manual_seed(rank)
     net = FastOthelloNet(8, 65)
@@ -47,11 +47,11 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _run(world):
+def _run(world, counts=(5, 0, 3)):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, counts)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -73,6 +73,15 @@ def test_replay_allgather_world2_bit_exact():
                 g = g.view(np.uint64)
             assert np.array_equal(g, exp), k
     assert res[0][3] == res[1][3]  # broadcast weights identical on every rank
+
+
+def test_replay_allgather_world2_no_rows_anywhere():
+    """A window in which no rank finished a move: counts [0, 0], no rows collective, empty
+    pooled rows on every rank."""
+    res = _run(2, counts=(0, 0))
+    for rank, cnts, got, w in res:
+        assert cnts == [0, 0]
+        assert all(len(got[k]) == 0 for k in ("own", "opp", "pi", "z", "player"))
 
 
 def test_pack_unpack_rows_edge_counts():
