@@ -499,8 +499,23 @@ struct FastTrunkArgs {
   int n_boards;
 };
 
+// four waves per SIMD: the register allocator fits the kernel into 128 VGPRs (accumulators
+// included, ten dwords spilled outside the main loops) so eight one-board workgroups share a CU
+// -- the LDS limit (8 x 18 KB) -- and a 2,048-board evaluation is one round of workgroups
+// instead of 1.33 rounds at six per CU (three waves: 120 VGPRs + 32 AGPRs): evaluation 105.7 ->
+// 97.7-98.4 us, configs[1] +2.6 % same box, same outputs (profiles/r06_c2_fast_trunk_waves_ab.json);
+// 0 = the allocator's own choice (A/B builds)
+#ifndef AZ_FT_WAVES
+#define AZ_FT_WAVES 4
+#endif
+#if AZ_FT_WAVES > 0
+#define AZ_FT_ATTR __attribute__((amdgpu_waves_per_eu(AZ_FT_WAVES)))
+#else
+#define AZ_FT_ATTR
+#endif
+
 template <class G>
-__global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
+__global__ __launch_bounds__(G::THREADS) AZ_FT_ATTR void k_fast_trunk(FastTrunkArgs a) {
   static_assert(G::BOARDS == 1 && G::SCALED, "one board per workgroup, FP16X2");
   constexpr int C = G::C, kThreads = G::THREADS;
   extern __shared__ float4 lds4[];
@@ -586,7 +601,7 @@ __global__ __launch_bounds__(G::THREADS) void k_fast_trunk(FastTrunkArgs a) {
   }
 
   f32x16 acc[G::TM];
-#pragma unroll  // three bodies: 116 VGPRs, three waves per SIMD (one body: 156, two)
+#pragma unroll  // three bodies (one rolled body needed 156 VGPRs)
   for (int layer = 0; layer < 3; ++layer) {
     const char* wq = a.wq[layer];
     mx_kloop<G>(acc, lds_a, wq, wlane, pos0, ok9, h, b0f, b1f, b2f, b3f);

@@ -357,4 +357,20 @@ c17() {
   done
   exit 0
 }
+c18() {
+  # FastOthelloNet's one-launch trunk at four waves per SIMD (exp6/ft4: amdgpu_waves_per_eu(4),
+  # 128 VGPRs, 8 workgroups per CU = one round of 2,048 boards) against three (6 per CU)
+  export OUT=gpurun_out/r06v
+  mkdir -p $OUT
+  run pytest_ft4 300 env AZ_LIB_PATH=exp6/ft4/libaz_othello.so python -u -m pytest tests/test_nn_gpu.py tests/test_net_golden_gpu.py -k "fast" -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread || exit $?
+  for i in 1 2 3; do
+    run net_prod 120 python scripts/net_time.py 2048 40 fast || exit $?
+    run net_ft4 120 env AZ_LIB_PATH=exp6/ft4/libaz_othello.so python scripts/net_time.py 2048 40 fast || exit $?
+  done
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_ft4 300 env AZ_LIB_PATH=exp6/ft4/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  exit 0
+}
 "$@"
