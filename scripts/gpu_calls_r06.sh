@@ -373,4 +373,16 @@ c18() {
   done
   exit 0
 }
+c19() {
+  # the arena's two engines on their own streams (AZ_ARENA_STREAMS, default on) against one
+  # stream: parity tests, then eval.py's matches at configs[2]'s net and sims, alternating
+  export OUT=gpurun_out/r06w
+  mkdir -p $OUT
+  pyt pytest_arena 600 tests/test_arena_gpu.py tests/test_callers_gpu.py || exit $?
+  for i in 1 2; do
+    run bench_arena 400 python bench.py --workload arena || exit $?
+    run bench_arena_1s 400 env AZ_ARENA_STREAMS=0 python bench.py --workload arena || exit $?
+  done
+  exit 0
+}
 "$@"
