@@ -193,6 +193,11 @@ f2() {
   run rocprof_default 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
     python3 bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
   rm -f $OUT/prof/run_kernel_trace.csv
+  if [ -n "$FIN_C2_PROF" ]; then
+    run rocprof_c2 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- \
+      python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000 --sustained-steps 0 --settle 0 || exit $?
+    rm -f $OUT/prof_c2/run_kernel_trace.csv
+  fi
   exit 0
 }
 
@@ -250,7 +255,7 @@ c11() {
 fin() {
   # the final tree: the whole GPU suite, smoke(), the driver's bench command and its kernel
   # summary, the other workloads' lines and configs[1]'s kernel summary
-  export OUT=gpurun_out/r06o
+  export OUT=${FIN_OUT:-gpurun_out/r06o}
   mkdir -p $OUT
   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
     --timeout-method thread || exit $?
@@ -264,6 +269,11 @@ fin() {
   run rocprof_default 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
     python3 bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu || exit $?
   rm -f $OUT/prof/run_kernel_trace.csv
+  if [ -n "$FIN_C2_PROF" ]; then
+    run rocprof_c2 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- \
+      python3 bench.py --workload c2 --skip-cpu --skip-kernel --steps 400 --warmup 2000 --sustained-steps 0 --settle 0 || exit $?
+    rm -f $OUT/prof_c2/run_kernel_trace.csv
+  fi
   exit 0
 }
 
