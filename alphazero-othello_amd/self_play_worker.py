@@ -6,6 +6,10 @@ the reference's signature so train.py's process pool (train.py:199-225) works un
 the game itself runs through the MCTS drop-in on the GPU engine.  `collect_self_play_games`
 is the batched replacement for that whole pool: one engine, G concurrent games on the GPU.
 """
+import os
+import shutil
+import time
+
 import numpy as np
 import torch
 
@@ -99,12 +103,164 @@ def _games_from_rows(rows):
     return games
 
 
+# one_self_play's shared generation (AZ_DROPIN_SHARED, default on when the args carry train.py's
+# num_self_play): the pool's workers coordinate through a directory named by the batch key
+# (policy weights + args: the same for every task of a generation).  The first worker to create
+# its `producer` file plays ALL num_self_play games in one batch on the GPU engine and publishes
+# the sample rows (rows.npz, written under another name and renamed into place, then `done`);
+# every call of every worker claims the next unclaimed game index with an O_EXCL file
+# (claim.<i>), so each game is handed out exactly once, in slot order of the one batch.  The
+# other workers never touch the GPU.  A worker that has read its game leaves read.<i>; the
+# reader that completes the set removes the directory.  A producer that died before `done`
+# (or failed: its waiters raise the error) has its directory retired -- renamed away -- and the
+# next caller produces anew.
+_SHARED = {"key": None, "games": None, "next": 0}
+
+
+def _shared_root():
+    """AZ_DROPIN_DIR, default .dropin_gen/ beside this module (inside the checkout)."""
+    return os.environ.get("AZ_DROPIN_DIR") or os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), ".dropin_gen")
+
+
+def _excl(path, text=""):
+    """Create `path` exclusively (atomic on a local file system); False if it exists."""
+    try:
+        fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o600)
+    except FileExistsError:
+        return False
+    with os.fdopen(fd, "w") as f:
+        f.write(text)
+    return True
+
+
+def _pid_alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+def _retire_stale(root, keep, max_age_s=600.0):
+    """Remove other generations' directories untouched for max_age_s (a generation whose
+    games were not all claimed -- e.g. a warm-up -- is never completed by its readers)."""
+    now = time.time()
+    for name in os.listdir(root):
+        path = os.path.join(root, name)
+        if name != keep:
+            try:
+                if now - os.stat(path).st_mtime > max_age_s:
+                    shutil.rmtree(path, ignore_errors=True)
+            except OSError:
+                pass
+
+
+def _shared_game(key, total, produce, poll_s=0.02):
+    """Game i of the generation `key` (total games, rows from produce(total)), or None when
+    every game has been claimed.  Returns a list of reference tuples."""
+    root = _shared_root()
+    os.makedirs(root, exist_ok=True)
+    name = key[:40]
+    d = os.path.join(root, name)
+    while True:
+        os.makedirs(d, exist_ok=True)
+        if _excl(os.path.join(d, "producer"), str(os.getpid())):
+            _retire_stale(root, name)
+            try:
+                rows = produce(total)
+                tmp = os.path.join(d, f"rows.{os.getpid()}.npz")
+                with open(tmp, "wb") as f:
+                    np.savez(f, **{k: np.asarray(v) for k, v in rows.items()})
+                os.replace(tmp, os.path.join(d, "rows.npz"))
+                tok = os.path.join(d, f"done.{os.getpid()}")
+                with open(tok, "w") as f:
+                    f.write(f"{os.getpid()}.{time.time_ns()}")
+                os.replace(tok, os.path.join(d, "done"))  # appears with its token
+            except BaseException as ex:
+                # waiters that see `failed` raise it; the directory is then retired, so a later
+                # call (or a waiter that missed it) produces anew
+                _excl(os.path.join(d, "failed"), repr(ex))
+                try:
+                    os.rename(d, f"{d}.failed.{os.getpid()}")
+                except OSError:
+                    pass
+                raise
+            break
+        retired = False
+        while not os.path.exists(os.path.join(d, "done")):
+            if not os.path.isdir(d):  # retired meanwhile: start over
+                retired = True
+                break
+            if os.path.exists(os.path.join(d, "failed")):
+                with open(os.path.join(d, "failed")) as f:
+                    raise RuntimeError(f"one_self_play: the generation's producer failed: {f.read()}")
+            try:
+                with open(os.path.join(d, "producer")) as f:
+                    pid = int(f.read() or 0)
+            except (OSError, ValueError):
+                pid = 0
+            if pid and not _pid_alive(pid):  # died before publishing: retire, start over
+                try:
+                    os.rename(d, f"{d}.dead.{pid}.{os.getpid()}")
+                except OSError:
+                    pass
+                retired = True
+                break
+            time.sleep(poll_s)
+        if not retired:
+            break
+    try:
+        with open(os.path.join(d, "done")) as f:
+            gen = (key, f.read())  # this publication (the same key can return in a later pool)
+    except FileNotFoundError:  # completed and removed meanwhile: every game was claimed
+        return None
+    if _SHARED["key"] != gen:
+        _SHARED.update(key=gen, games=None, next=0)
+    for i in range(_SHARED["next"], total):
+        if _excl(os.path.join(d, f"claim.{i}"), str(os.getpid())):
+            break
+    else:
+        return None
+    _SHARED["next"] = i + 1
+    if _SHARED["games"] is None:
+        with np.load(os.path.join(d, "rows.npz")) as z:
+            _SHARED["games"] = _games_from_rows({k: z[k] for k in z.files})
+    game = _SHARED["games"][i]
+    _excl(os.path.join(d, f"read.{i}"))
+    try:
+        if sum(n.startswith("read.") for n in os.listdir(d)) == total:
+            shutil.rmtree(d, ignore_errors=True)
+    except OSError:
+        pass
+    return game
+
+
+def _shared_total(args):
+    """The generation's game count when one_self_play shares it (AZ_DROPIN_SHARED, default
+    on): train.py's num_self_play from the args; None = per-worker batches."""
+    if os.environ.get("AZ_DROPIN_SHARED", "1") != "1":
+        return None
+    try:
+        total = int((args or {})["num_self_play"])
+    except (KeyError, TypeError, ValueError):
+        return None
+    return total if total > 0 else None
+
+
 @torch.no_grad()
 def one_self_play(args_tuple):
     """One complete game (self_play_worker.py:38-88); returns [(state, pi, G)].
 
     train.py's spawn pool (train.py:199-225) calls this once per game in each worker
-    process.  By default (AZ_DROPIN_BATCH = 32, capped at the worker's share
+    process.  When the args carry train.py's num_self_play (AZ_DROPIN_SHARED, default on),
+    the pool's workers share ONE batch of that many games: the first call of the generation
+    plays all of them on the GPU engine and every call returns the next unclaimed one
+    (_shared_game: one producer, the other workers never touch the GPU; coordination files
+    under AZ_DROPIN_DIR, default .dropin_gen/ beside this module).  Otherwise
+    (AZ_DROPIN_BATCH = 32, capped at the worker's share
     ceil(num_self_play / num_workers) when args carry them) the worker's first call plays that
     many games at once on the batched GPU engine (BatchedSelfPlay: the same search, K =
     args['num_threads'] virtual-loss leaves per step, Dirichlet root noise, temperature
@@ -117,9 +273,25 @@ def one_self_play(args_tuple):
     board_size, args, policy_state, _ = args_tuple
     if _dropin_batch_size() <= 1:
         return _one_game(args_tuple)
-    n = _dropin_batch_size(args)
     assert board_size == 8
     key = _batch_key(board_size, args, policy_state)
+    total = _shared_total(args)
+    if total is not None:
+        def produce(n):
+            policy_class, policy_config, policy_state_dict = policy_state
+            policy = policy_class(**policy_config)
+            policy.load_state_dict(policy_state_dict)
+            policy.eval()
+            seed = int(np.random.randint(0, 2**31 - 1))
+            rows = _local_rows(policy, args, n, None, seed, 0, False, torch.float32)
+            assert len(_games_from_rows(rows)) == n
+            return rows
+
+        game = _shared_game(key, total, produce)
+        if game is not None:
+            return game
+        # more calls than the generation's games: this worker's own batches from here on
+    n = _dropin_batch_size(args)
     if _BATCH["key"] != key:
         _BATCH["key"], _BATCH["games"] = key, []
     if not _BATCH["games"]:

@@ -5,7 +5,11 @@ GPU engine (its own HIP context, one game at a time, the fused HIP net).  Small 
 kernels from several workers run side by side on the GPU's CUs, so the pool scales with the
 worker count until the card is shared out.
 
-    python scripts/dropin_pool_bench.py [workers] [games] [sims] > out.json
+    python scripts/dropin_pool_bench.py [workers] [games] [sims] [cold] > out.json
+
+cold: no warm-up -- the timed region is train.py's whole `with Pool(...)` block (worker start,
+imports, the HIP context and graph capture of whichever worker plays) as one generation of
+train.py pays it.
 
 Each worker plays one short warm-up game in its initializer (HIP context, kernels, graph
 capture), then the timed batch of `games` games is streamed through imap_unordered with
@@ -63,12 +67,21 @@ def main():
     args = {"c_puct": 2.0, "num_simulations": sims, "dirichlet_alpha": 1.0,
             "dirichlet_epsilon": 0.3, "mcts_temperature": 1.0, "num_exploratory_moves": 35,
             "lambda": 0.98, "num_self_play": games, "num_workers": workers}
+    cold = len(sys.argv) > 4 and sys.argv[4] == "cold"
     ctx = get_context("spawn")
-    with ctx.Pool(workers, initializer=_init) as pool:
-        pool.map(_play, [(8, dict(args, num_simulations=8), ps, None)] * workers)  # all warm
+    if cold:
         t0 = time.perf_counter()
-        lens = list(pool.imap_unordered(_play, [(8, args, ps, None)] * games, chunksize=1))
+        with ctx.Pool(workers) as pool:
+            lens = list(pool.imap_unordered(_play, [(8, args, ps, None)] * games, chunksize=1))
         dt = time.perf_counter() - t0
+    else:
+        with ctx.Pool(workers, initializer=_init) as pool:
+            # warm-up tasks (8 sims, without num_self_play: each worker's own batch)
+            warm = {k: v for k, v in args.items() if k != "num_self_play"}
+            pool.map(_play, [(8, dict(warm, num_simulations=8), ps, None)] * workers)
+            t0 = time.perf_counter()
+            lens = list(pool.imap_unordered(_play, [(8, args, ps, None)] * games, chunksize=1))
+            dt = time.perf_counter() - t0
     plies = sum(lens)
     print(json.dumps({"workers": workers, "games": games, "sims": sims,
                       "games_per_s": round(games / dt, 4), "plies": plies,
@@ -80,7 +93,10 @@ def main():
                       "path": "train.py Pool -> one_self_play (AZ_DROPIN_BATCH games per worker "
                               "batch on the batched engine; 1 = one game per call through the "
                               "drop-in MCTS), 4 leaves/step",
-                      "dropin_batch": int(os.environ.get("AZ_DROPIN_BATCH", "32"))}))
+                      "dropin_batch": int(os.environ.get("AZ_DROPIN_BATCH", "32")),
+                      "shared_generation": os.environ.get("AZ_DROPIN_SHARED", "1") == "1",
+                      "timed": "the whole Pool block (cold)" if cold else
+                               "imap_unordered over warm workers"}))
 
 
 if __name__ == "__main__":
