@@ -395,4 +395,16 @@ c19() {
   done
   exit 0
 }
+c20() {
+  # unchanged train.py's pool at the reference's num_self_play = 300 over 15 workers: the
+  # shared generation (one producer plays all 300 games) against per-worker batches
+  # (AZ_DROPIN_SHARED=0), warm workers; then the whole Pool block cold (one generation as
+  # train.py pays it, worker start and HIP context included)
+  export OUT=gpurun_out/r06y
+  mkdir -p $OUT
+  run pool_shared 600 python scripts/dropin_pool_bench.py 15 300 400 || exit $?
+  run pool_perworker 600 env AZ_DROPIN_SHARED=0 python scripts/dropin_pool_bench.py 15 300 400 || exit $?
+  run pool_shared_cold 600 python scripts/dropin_pool_bench.py 15 300 400 cold || exit $?
+  exit 0
+}
 "$@"
