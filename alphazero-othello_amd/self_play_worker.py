@@ -283,7 +283,9 @@ def one_self_play(args_tuple):
             policy.load_state_dict(policy_state_dict)
             policy.eval()
             seed = int(np.random.randint(0, 2**31 - 1))
-            rows = _local_rows(policy, args, n, None, seed, 0, False, torch.float32)
+            # AZ_DROPIN_PIPELINES (experiments): the generation's slots as that many pipelines
+            pipes = int(os.environ.get("AZ_DROPIN_PIPELINES", "1"))
+            rows = _local_rows(policy, args, n, None, seed, 0, False, torch.float32, pipes)
             assert len(_games_from_rows(rows)) == n
             return rows
 

@@ -407,4 +407,15 @@ c20() {
   run pool_shared_cold 600 python scripts/dropin_pool_bench.py 15 300 400 cold || exit $?
   exit 0
 }
+c21() {
+  # the shared generation's producer as one pipeline (default) or two (AZ_DROPIN_PIPELINES=2:
+  # 2 x 150 slots, each evaluation 600 rows in one trunk launch instead of 1,024 + 176), cold
+  export OUT=gpurun_out/r06z
+  mkdir -p $OUT
+  for i in 1 2; do
+    run pool_cold_p1 600 python scripts/dropin_pool_bench.py 15 300 400 cold || exit $?
+    run pool_cold_p2 600 env AZ_DROPIN_PIPELINES=2 python scripts/dropin_pool_bench.py 15 300 400 cold || exit $?
+  done
+  exit 0
+}
 "$@"
