@@ -146,16 +146,24 @@ def _pid_alive(pid):
 
 def _retire_stale(root, keep, max_age_s=600.0):
     """Remove other generations' directories untouched for max_age_s (a generation whose
-    games were not all claimed -- e.g. a warm-up -- is never completed by its readers)."""
+    games were not all claimed -- e.g. a warm-up -- is never completed by its readers), except
+    one whose producer is still alive and playing (no `done` yet)."""
     now = time.time()
     for name in os.listdir(root):
         path = os.path.join(root, name)
-        if name != keep:
-            try:
-                if now - os.stat(path).st_mtime > max_age_s:
-                    shutil.rmtree(path, ignore_errors=True)
-            except OSError:
-                pass
+        if name == keep or not os.path.isdir(path):
+            continue
+        try:
+            if now - os.stat(path).st_mtime <= max_age_s:
+                continue
+            if not os.path.exists(os.path.join(path, "done")):
+                with open(os.path.join(path, "producer")) as f:
+                    pid = int(f.read() or 0)
+                if pid and _pid_alive(pid):
+                    continue
+        except (OSError, ValueError):
+            pass
+        shutil.rmtree(path, ignore_errors=True)
 
 
 def _shared_game(key, total, produce, poll_s=0.02):

@@ -141,6 +141,23 @@ def test_failed_producer_is_reported(scratch, monkeypatch):
         spw._shared_game("e" * 40, 3, lambda n: _fake_rows(n))
 
 
+def test_stale_generations_are_retired_but_not_live_producers(scratch):
+    root = scratch / "gen"
+    old_done, old_dead, old_live = (root / n for n in ("a" * 40, "b" * 40, "c" * 40))
+    for d in (old_done, old_dead, old_live):
+        d.mkdir(parents=True)
+    (old_done / "done").write_text("x")
+    p = mp.get_context("spawn").Process(target=int)
+    p.start()
+    p.join()
+    (old_dead / "producer").write_text(str(p.pid))
+    (old_live / "producer").write_text(str(os.getpid()))  # still playing
+    for d in (old_done, old_dead, old_live):
+        os.utime(d, (0, 0))
+    spw._retire_stale(str(root), "z" * 40)
+    assert not old_done.exists() and not old_dead.exists() and old_live.exists()
+
+
 def test_shared_total_from_args(monkeypatch):
     assert spw._shared_total({"num_self_play": 300, "num_workers": 15}) == 300
     assert spw._shared_total({"num_workers": 15}) is None
