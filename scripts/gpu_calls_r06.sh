@@ -418,4 +418,14 @@ c21() {
   done
   exit 0
 }
+fin2() {
+  # the final tree once more: the GPU suite, smoke(), the driver's command
+  export OUT=gpurun_out/r06zz
+  mkdir -p $OUT
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread || exit $?
+  run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+  run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+  exit 0
+}
 "$@"
