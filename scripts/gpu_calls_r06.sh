@@ -428,4 +428,13 @@ fin2() {
   run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
   exit 0
 }
+c22() {
+  # configs[1]'s evaluation by part, each alone (scripts/fast_parts_time.py)
+  export OUT=gpurun_out/r06aa
+  mkdir -p $OUT
+  for i in 1 2; do
+    run parts 120 python scripts/fast_parts_time.py 2048 30 || exit $?
+  done
+  exit 0
+}
 "$@"
