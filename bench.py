@@ -1008,7 +1008,7 @@ def main():
         rt = trunk_roofline(sp, device, lb)  # above 4 x CUs boards: one launch per chunk
         if rt is not None:
             result["roofline_trunk"] = rt
-    if rank == 0 and not a.skip_cpu:
+    if rank == 0 and world == 1 and not a.skip_cpu:  # the contract: rank 0 at N = 1 only
         result["cpu_baseline"] = cpu_baseline_pool(a.net, a.sims, a.cpu_seconds,
                                                    a.cpu_workers or host_cpu_share())
     if rank == 0:
