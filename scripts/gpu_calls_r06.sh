@@ -437,4 +437,15 @@ c22() {
   done
   exit 0
 }
+c23() {
+  # bench.py's N > 1 path rehearsed on the one-GPU box with the final bench.py (the driver's
+  # torchrun shape, world 2, every rank on cuda:0, gloo collectives; no --skip-cpu: rank 0
+  # must leave cpu_baseline out at N > 1), then the driver's N = 1 command
+  export OUT=gpurun_out/r06ab
+  mkdir -p $OUT
+  run rehearse_w2 400 env AZ_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 || exit $?
+  run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+  exit 0
+}
 "$@"
