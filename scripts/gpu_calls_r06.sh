@@ -448,4 +448,19 @@ c23() {
   run bench_default 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
   exit 0
 }
+c24() {
+  # LLVM scheduling strategies for the trunk sources (conv_wino4.hip, conv16.hip): max-ilp,
+  # max-memory-clause, iterative-ilp against the default, alternating: configs[2]'s evaluation
+  # (net_time 1024) and configs[1]'s by part (fast_parts_time 2048)
+  export OUT=gpurun_out/r06ac
+  mkdir -p $OUT
+  for i in 1 2; do
+    for v in prod silp smem sitl; do
+      if [ $v = prod ]; then L=""; else L="AZ_LIB_PATH=exp6/$v/libaz_othello.so"; fi
+      run net_$v 120 env $L python scripts/net_time.py 1024 40 || exit $?
+      run fast_$v 120 env $L python scripts/fast_parts_time.py 2048 30 || exit $?
+    done
+  done
+  exit 0
+}
 "$@"
