@@ -463,4 +463,12 @@ c24() {
   done
   exit 0
 }
+c25() {
+  # counters of FastOthelloNet's one-launch trunk (scripts/pmc_fast_trunk.sh)
+  export OUT=gpurun_out/r06ad
+  mkdir -p $OUT
+  bash scripts/pmc_fast_trunk.sh || exit $?
+  SQ_KERNEL=k_fast_trunk python scripts/sq_summary.py $OUT/sq_fast > $OUT/sq_fast_summary.txt || exit $?
+  exit 0
+}
 "$@"
