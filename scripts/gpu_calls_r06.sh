@@ -471,4 +471,20 @@ c25() {
   SQ_KERNEL=k_fast_trunk python scripts/sq_summary.py $OUT/sq_fast > $OUT/sq_fast_summary.txt || exit $?
   exit 0
 }
+c26() {
+  # the fast trunk's epilogue image stores as channel pairs (exp6/pairw) against 16-bit stores:
+  # bit-identity tests with the variant, evaluation parts and configs[1] A/B
+  export OUT=gpurun_out/r06ae
+  mkdir -p $OUT
+  run pytest_pairw 300 env AZ_LIB_PATH=exp6/pairw/libaz_othello.so python -u -m pytest tests/test_nn_gpu.py tests/test_net_golden_gpu.py -k "fast" -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread || exit $?
+  for i in 1 2 3; do
+    run fast_prod 120 python scripts/fast_parts_time.py 2048 30 || exit $?
+    run fast_pairw 120 env AZ_LIB_PATH=exp6/pairw/libaz_othello.so python scripts/fast_parts_time.py 2048 30 || exit $?
+  done
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_pairw 300 env AZ_LIB_PATH=exp6/pairw/libaz_othello.so python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  exit 0
+}
 "$@"
