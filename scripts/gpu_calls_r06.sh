@@ -487,4 +487,18 @@ c26() {
   done
   exit 0
 }
+c27() {
+  # the heads GEMM at 4 K slices (256 workgroups, one per CU) against 8, by part and configs[1]
+  export OUT=gpurun_out/r06af
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    run fast_s8 120 python scripts/fast_parts_time.py 2048 30 || exit $?
+    run fast_s4 120 env AZ_FAST_GEMM_SPLITS=4 python scripts/fast_parts_time.py 2048 30 || exit $?
+  done
+  for i in 1 2; do
+    run bench_c2 300 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+    run bench_c2_s4 300 env AZ_FAST_GEMM_SPLITS=4 python bench.py --workload c2 --skip-cpu --skip-kernel || exit $?
+  done
+  exit 0
+}
 "$@"
