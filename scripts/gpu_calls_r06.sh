@@ -501,4 +501,17 @@ c27() {
   done
   exit 0
 }
+c28() {
+  # non-temporal hints in the resident persistent trunk (AZ_W4_NT: 1 = the residual's LDS-DMA
+  # reads, 2 = the output stores, 3 = both) against none, configs[2]'s evaluation, alternating
+  export OUT=gpurun_out/r06ag
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    for v in prod nt1 nt2 nt3; do
+      if [ $v = prod ]; then L=""; else L="AZ_LIB_PATH=exp6/$v/libaz_othello.so"; fi
+      run net_$v 120 env $L python scripts/net_time.py 1024 40 || exit $?
+    done
+  done
+  exit 0
+}
 "$@"
