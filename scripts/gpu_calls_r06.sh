@@ -514,4 +514,16 @@ c28() {
   done
   exit 0
 }
+c29() {
+  # configs[4]'s fp16 persistent trunk: weight prefetch distance (AZ_W4_PD16) 3 / 5 against 7
+  export OUT=gpurun_out/r06ah
+  mkdir -p $OUT
+  for i in 1 2 3; do
+    for v in prod pd16_3 pd16_5; do
+      if [ $v = prod ]; then L=""; else L="AZ_LIB_PATH=exp6/$v/libaz_othello.so"; fi
+      run net16_$v 120 env $L python scripts/net_time.py 1024 40 fp16 || exit $?
+    done
+  done
+  exit 0
+}
 "$@"
